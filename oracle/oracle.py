@@ -1,0 +1,154 @@
+"""ctypes wrapper around oracle/libikoracle.so (the C restatement) plus the
+numpy ANN restatement.
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the parity checker; the product package
+(inversekinematicsann_amd) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libikoracle.so")
+_lib = None
+
+OK, E_OUT_OF_REACH, E_DOMAIN, E_ZERODIV, E_ANGLE_RANGE = 0, 1, 2, 3, 4
+
+# robot/robot.py:38-42 (SixDOFRobot), restated as plain data.
+PI = 3.141592653589793
+DH = np.array([[0.0, PI / 2, 0.0, 0.0], [2.0, 0.0, 0.0, 0.0], [0.0, 2.0, 2.0, 2.0],
+               [PI / 2, 0.0, 0.0, 0.0]], dtype=np.float64)
+LINKS = np.array([2.0, 2.0, 2.0, 2.0], dtype=np.float64)
+LIMITS = np.array([0.0, 6.0, -6.0, 6.0, -3.0, 6.0], dtype=np.float64)
+
+
+def build(quiet: bool = True) -> str:
+    """Compile libikoracle.so with the committed Makefile (gcc)."""
+    out = subprocess.run(["make", "-C", _HERE], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+    if not quiet:
+        print(out.stdout)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        dp = ctypes.POINTER(ctypes.c_double)
+        ip = ctypes.POINTER(ctypes.c_int32)
+        i64 = ctypes.c_int64
+        L.iko_round_nd.argtypes = [ctypes.c_double, ctypes.c_int]
+        L.iko_round_nd.restype = ctypes.c_double
+        L.iko_set_fma_chain.argtypes = [ctypes.c_int]
+        L.iko_fk.argtypes = [dp, dp, i64, dp, dp, ip]
+        L.iko_fabrik_calc.argtypes = [ctypes.c_int, dp, dp, dp, i64, ctypes.c_double,
+                                      ctypes.c_int, dp, ip, ip]
+        L.iko_check_limits.argtypes = [dp, dp, i64]
+        L.iko_check_limits.restype = i64
+        L.iko_fabrik_ikine.argtypes = [dp, dp, dp, i64, ctypes.c_double, ctypes.c_int, dp,
+                                       ip, dp, ip]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _i(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def round_nd(v: float, nd: int = 8) -> float:
+    return lib().iko_round_nd(float(v), nd)
+
+
+def fk(angles, dh=DH):
+    """Batch ForwardKinematics.fkine: returns (effector xyz n x 3, joints n x 4 x 3, status)."""
+    a = np.ascontiguousarray(angles, dtype=np.float64).reshape(-1, 4)
+    n = a.shape[0]
+    xyz = np.empty((n, 3)); joints = np.empty((n, 4, 3)); st = np.empty(n, np.int32)
+    dh = np.ascontiguousarray(dh, dtype=np.float64)
+    lib().iko_fk(_d(dh), _d(a), n, _d(xyz), _d(joints), _i(st))
+    return xyz, joints, st
+
+
+def check_limits(pts, limits=LIMITS) -> int:
+    p = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 3)
+    lim = np.ascontiguousarray(limits, dtype=np.float64)
+    return int(lib().iko_check_limits(_d(lim), _d(p), p.shape[0]))
+
+
+def fabrik_ikine(pts, tol=1e-3, max_iter=100, dh=DH, links=LINKS):
+    """FabrikInverseKinematics.ikine restated (limits not checked here).
+    Returns (angles n x 4, iters n, joints n x 4 x 3, status n)."""
+    p = np.ascontiguousarray(pts, dtype=np.float64).reshape(-1, 3)
+    n = p.shape[0]
+    ang = np.empty((n, 4)); it = np.empty(n, np.int32); jo = np.empty((n, 4, 3))
+    st = np.empty(n, np.int32)
+    dh = np.ascontiguousarray(dh, dtype=np.float64)
+    links = np.ascontiguousarray(links, dtype=np.float64)
+    lib().iko_fabrik_ikine(_d(dh), _d(links), _d(p), n, float(tol), int(max_iter), _d(ang),
+                           _i(it), _d(jo), _i(st))
+    return ang, it, jo, st
+
+
+def fabrik_calc(init, goals, dists=LINKS, tol=1e-3, max_iter=100):
+    """Batch Fabrik.calculate: init n x nj x 3, goals n x 3 -> (joints, iters, status)."""
+    init = np.ascontiguousarray(init, dtype=np.float64)
+    n, nj, _ = init.shape
+    g = np.ascontiguousarray(goals, dtype=np.float64).reshape(n, 3)
+    d = np.ascontiguousarray(dists, dtype=np.float64)
+    out = np.empty_like(init); it = np.empty(n, np.int32); st = np.empty(n, np.int32)
+    lib().iko_fabrik_calc(nj, _d(d), _d(init), _d(g), n, float(tol), int(max_iter), _d(out),
+                          _i(it), _i(st))
+    return out, it, st
+
+
+# ------------------------------------------------------------------ ANN ----
+def ann_forward(points, weights, biases, acts, x_mean, x_scale, y_mean, y_scale,
+                compute=np.float64):
+    """ANN.predict restated (kinematics/ann.py:70-76).
+
+    scale_x: sklearn StandardScaler.transform in float64 ((p - mean) / scale),
+    then Keras casts to float32; Dense layers compute x @ W + b then the
+    activation (ann.py:46-56); the output is float32 and is inverse-scaled in
+    place (Y *= scale; Y += mean, each op in float64 rounded back to float32,
+    as numpy does for an in-place float32 op with a float64 operand).
+    `compute` selects the dtype of the MLP itself (float64 reference or float32).
+    """
+    p = np.asarray(points, dtype=np.float64).reshape(-1, 3)
+    x = (p - np.asarray(x_mean, np.float64)) / np.asarray(x_scale, np.float64)
+    h = x.astype(np.float32).astype(compute)
+    for W, b, a in zip(weights, biases, acts):
+        h = h @ np.asarray(W, compute) + np.asarray(b, compute)
+        if a == "tanh":
+            h = np.tanh(h)
+        elif a == "relu":
+            h = np.maximum(h, 0)
+        elif a == "sigmoid":
+            h = 1 / (1 + np.exp(-h))
+        elif a != "linear":
+            raise ValueError(a)
+    y = h.astype(np.float32)
+    y = (y.astype(np.float64) * np.asarray(y_scale, np.float64)).astype(np.float32)
+    y = (y.astype(np.float64) + np.asarray(y_mean, np.float64)).astype(np.float32)
+    return y
+
+
+def fk_closed_form(angles):
+    """Closed-form effector position of the SixDOFRobot chain in float64."""
+    a = np.asarray(angles, np.float64).reshape(-1, 4)
+    t1, t2, t3, t4 = a[:, 0], a[:, 1], a[:, 2], a[:, 3]
+    r = 2 * np.cos(t2) + 2 * np.cos(t2 + t3) + 2 * np.cos(t2 + t3 + t4)
+    z = 2 + 2 * np.sin(t2) + 2 * np.sin(t2 + t3) + 2 * np.sin(t2 + t3 + t4)
+    return np.stack([np.cos(t1) * r, np.sin(t1) * r, z], axis=1)
