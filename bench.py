@@ -1,0 +1,303 @@
+"""Benchmark: IK solutions/s of the MI355X engine (BASELINE.json metric).
+
+Default workload (BASELINE.json configs[1]): ANN MLP forward of the reference
+architecture (ann.py:46-56: 3 -> 12 x Dense(500, tanh) -> Dense(4)) over 1M
+random_dist points per GPU in fp32, with the FK round-trip error fused in the
+same launch.  `--method fabrik` measures configs[2] (FABRIK, tol 1e-3 /
+100 iterations, float64).  One step = one solve of the whole per-GPU batch with
+inputs already resident in HBM.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--method ann|fabrik]
+
+N > 1 is launched one process per GPU (torch.distributed.run); the batch is
+sharded by point (weak scaling: each rank solves its own 1M points, no
+collective on the data path); the step time is the max over ranks.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "IK solutions/sec (6DOF, 1M-point batch) at 1/2/4/8 GPUs; max |FK err|"
+ANN_DIMS = (3,) + (500,) * 12 + (4,)
+FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: dense fp32 matrix peak
+FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
+HBM_PEAK = 8.0e12           # bytes/s
+FABRIK_FLOP_PER_ITER = 132
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--method", choices=["ann", "fabrik"], default="ann")
+    ap.add_argument("--points", type=int, default=1_000_000, help="points per GPU")
+    ap.add_argument("--tol", type=float, default=1e-3)
+    ap.add_argument("--max-iter", type=int, default=100)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="CPU-baseline time budget (rank 0, N=1); 0 disables")
+    ap.add_argument("--secondary", type=int, default=1,
+                    help="also time the other method and report it under 'secondary'")
+    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(v: float, world: int) -> float:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(v: float, world: int) -> float:
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def load_traffic(path, kernel):
+    """HBM bytes per launch of `kernel` from the PMC pass (tools/pmc_traffic.py),
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; None if not collected."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def run_ann(ctx, dpts, n, args, world):
+    import torch
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.kinematics.ann import (REFERENCE_X_SCALER as XS,
+                                                         REFERENCE_Y_SCALER as YS, glorot_model)
+    m = glorot_model(ANN_DIMS, seed=0)
+    ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    dang = torch.empty((n, 4), dtype=torch.float32, device="cuda")
+    derr = torch.empty(n, dtype=torch.float64, device="cuda")
+    flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
+
+    def step():
+        ctx.ann_solve_device(dpts, dang, derr, flags=flags)
+
+    res = timed(ctx, step, args, world)
+    st = ctx.stats_fetch()
+    res["max_fk_err"] = max_over_ranks(st.max_fk_err, world)
+    res["mean_fk_err"] = sum_over_ranks(st.sum_fk_err, world) / (n * world)
+    flop_pt = m.flops_per_point()
+    k = res["kernels"].get("ann_fused_kernel")
+    achieved = flop_pt * n / (k / 1e3) if k else None
+    traffic = load_traffic(args.traffic_file, "ann_fused_kernel")
+    res["roofline"] = {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
+                       "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+                       "frac": achieved / FP32_MFMA_PEAK if achieved else None,
+                       "traffic": traffic, "kernel": "ann_fused_kernel",
+                       "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
+                       "points_per_launch": n}
+    res["dtype"] = "fp32"
+    res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
+                       "1M random_dist points per GPU")
+    return res
+
+
+def run_fabrik(ctx, dpts, n, args, world):
+    import torch
+    from inversekinematicsann_amd import _native
+    dang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
+    dit = torch.empty(n, dtype=torch.int32, device="cuda")
+    flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
+
+    def step():
+        ctx.fabrik_solve_device(dpts, dang, dit, None, args.tol, args.max_iter, flags=flags)
+
+    res = timed(ctx, step, args, world)
+    st = ctx.stats_fetch()
+    res["mean_iters"] = st.sum_iters / n
+    res["n_capped"] = st.n_capped
+    k = res["kernels"].get("fabrik_iter_kernel")
+    flops = FABRIK_FLOP_PER_ITER * st.sum_iters
+    achieved = flops / (k / 1e3) if k else None
+    traffic = load_traffic(args.traffic_file, "fabrik_iter_kernel")
+    res["roofline"] = {"bound": "valu_fp64", "achieved": achieved / 1e12 if achieved else None,
+                       "peak": FP64_VALU_PEAK / 1e12, "unit": "TFLOP/s",
+                       "frac": achieved / FP64_VALU_PEAK if achieved else None,
+                       "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
+                       "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
+                       "iterations_per_launch": int(st.sum_iters)}
+    res["dtype"] = "f64"
+    res["workload"] = (f"FABRIK ikine (seed FK + loop + angles), tol {args.tol:g} / "
+                       f"{args.max_iter} iterations, float64, 1M random_dist points per GPU")
+    return res
+
+
+def timed(ctx, step, args, world):
+    import torch
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # per-kernel HIP-event durations of one representative step
+    ctx.set_timing(True)
+    step()
+    kernels = {}
+    for name, ms in ctx.kernel_times():
+        kernels[name] = kernels.get(name, 0.0) + ms
+    ctx.set_timing(False)
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    wall = max_over_ranks(wall, world)
+    ev_ms = ev0.elapsed_time(ev1) / args.steps
+    return {"wall_s": wall, "ms_per_step": wall * 1e3 / args.steps, "event_ms_per_step": ev_ms,
+            "kernels": kernels}
+
+
+def cpu_baseline(method, args):
+    """The oracle timed on this host (rank 0, N=1) over a bounded sample."""
+    from oracle import oracle as O
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    budget = args.cpu_seconds
+    if method == "ann":
+        try:
+            from threadpoolctl import threadpool_info
+            threads = max([i.get("num_threads", 1) for i in threadpool_info()
+                           if i.get("user_api") == "blas"] or [1])
+        except Exception:  # noqa: BLE001
+            threads = os.cpu_count() or 1
+        from inversekinematicsann_amd.kinematics.ann import (REFERENCE_X_SCALER as XS,
+                                                             REFERENCE_Y_SCALER as YS,
+                                                             glorot_model)
+        m = glorot_model(ANN_DIMS, seed=0)
+        chunk = 8192
+        pts = random_dist(chunk, seed=99)
+        done, t0 = 0, time.perf_counter()
+        while True:
+            O.ann_forward(pts, m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean,
+                          YS.scale, compute=np.float32)
+            done += chunk
+            if time.perf_counter() - t0 >= budget:
+                break
+        el = time.perf_counter() - t0
+        return {"value": done / el, "unit": "IK solutions/s", "cores": threads, "kind": "port",
+                "sample": f"{done} random_dist points in {chunk}-point batches, numpy fp32 MLP "
+                          f"(oracle.ann_forward) on {threads} BLAS threads, {el:.1f} s"}
+    chunk = 4096
+    pts = random_dist(chunk, seed=99)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        O.fabrik_ikine(pts, args.tol, args.max_iter)
+        done += chunk
+        if time.perf_counter() - t0 >= budget:
+            break
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "IK solutions/s", "cores": 1, "kind": "port",
+            "sample": f"{done} random_dist points, C oracle (oracle/ik_oracle.c, scalar, "
+                      f"1 thread), tol {args.tol:g}/{args.max_iter}, {el:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    world, rank, local = dist_setup(args)
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    n = args.points
+    pts = random_dist(n, seed=rank)  # rank r solves shard r of the N x 1M global batch
+    dpts = torch.from_numpy(pts).cuda()
+    ctx = _native.Context(local)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    runners = {"ann": run_ann, "fabrik": run_fabrik}
+    res = runners[args.method](ctx, dpts, n, args, world)
+    secondary = {}
+    if args.secondary:
+        other = "fabrik" if args.method == "ann" else "ann"
+        r2 = runners[other](ctx, dpts, n, args, world)
+        secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
+                            "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
+                            "roofline": r2["roofline"], "workload": r2["workload"],
+                            **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "mean_iters",
+                                                  "n_capped") if k in r2}}
+    total = n * world
+    value = total / (res["ms_per_step"] / 1e3)
+    line = {
+        "metric": METRIC, "value": value, "unit": "IK solutions/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": res["dtype"],
+        "data": "synthetic: random_dist points (truncated normal sd 0.5 in the workspace box, "
+                "seed = rank); ANN weights random Glorot-uniform of the reference architecture "
+                "(the reference .h5 is not shipped); reference StandardScaler constants",
+        "config": {"workload": res["workload"], "points_per_gpu": n, "total_points": total,
+                   "parallelism": f"dp{world}", "method": args.method,
+                   "tol": args.tol if args.method == "fabrik" else None,
+                   "max_iter": args.max_iter if args.method == "fabrik" else None},
+        "roofline": res["roofline"],
+        "event_ms_per_step": res["event_ms_per_step"],
+        "kernels_ms": res["kernels"],
+    }
+    for k in ("max_fk_err", "mean_fk_err", "mean_iters", "n_capped"):
+        if k in res:
+            line[k] = res[k]
+    if secondary:
+        line["secondary"] = secondary
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_baseline(args.method, args)
+        if args.secondary:
+            other = "fabrik" if args.method == "ann" else "ann"
+            line["secondary"][other]["cpu_baseline"] = cpu_baseline(other, args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

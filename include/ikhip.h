@@ -1,0 +1,141 @@
+/*
+ * ikhip.h -- C ABI of libikhip.so, the MI355X (gfx950) batched inverse-kinematics
+ * engine.  Plain pointers and sizes only; no torch or HIP types in the
+ * signatures (streams are passed as void*, a hipStream_t underneath).
+ *
+ * Each entry point replaces one function of the reference
+ * (lstar93/InverseKinematicsANN, file:line below).  The reference is pure
+ * Python and has no FFI of its own; the binding a maintainer would add on the
+ * reference side is a ctypes stub, shown in INTEGRATION.md.
+ *
+ * Pointer convention: by default every array argument is a HOST pointer and the
+ * call blocks until results are back in host memory.  With IK_F_DEVICE the
+ * array arguments are device pointers (e.g. torch tensors' data_ptr()) on the
+ * context's device, and with IK_F_ASYNC the call only enqueues work on the
+ * context's stream (stats are then read with ik_stats_fetch()).
+ *
+ * Error convention: every call returns an ik_status.  Per-point failures of the
+ * reference (its exceptions) are NOT call failures: they are reported in
+ * ik_stats (first_oob / first_err / first_err_code) so that the host can raise
+ * the reference's exception for the lowest failing index, exactly as the
+ * reference's sequential loop would.  Calls on one context are not re-entrant.
+ */
+#ifndef IKHIP_H
+#define IKHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum ik_status {
+  IK_OK = 0,
+  IK_E_OUT_OF_REACH = 1, /* OutOfRobotReachException, kinematics/inverse.py:32 */
+  IK_E_DOMAIN = 2,       /* ValueError('math domain error'), acos in inverse.py:81,92,100 */
+  IK_E_ZERODIV = 3,      /* ZeroDivisionError, kinematics/point.py:40, inverse.py:81,92,100 */
+  IK_E_ANGLE_RANGE = 4,  /* OutOfRobotReachException, kinematics/forward.py:23-25 */
+  IK_E_BADARG = 16,      /* invalid argument (shape/size/order of calls) */
+  IK_E_HIP = 17,         /* HIP runtime failure (see ik_last_error) */
+  IK_E_NOMODEL = 18      /* ik_ann_solve before ik_ann_load */
+} ik_status;
+
+enum {
+  IK_F_DEVICE = 1,    /* array arguments are device pointers */
+  IK_F_ASYNC = 2,     /* enqueue only; requires IK_F_DEVICE */
+  IK_F_NO_LIMITS = 4  /* skip the workspace check (ANN.predict has none, ann.py:70-76) */
+};
+
+enum { IK_ACT_LINEAR = 0, IK_ACT_TANH = 1, IK_ACT_RELU = 2, IK_ACT_SIGMOID = 3 };
+
+typedef struct ik_ctx ik_ctx;
+
+typedef struct ik_stats {
+  int64_t first_oob;      /* lowest index outside the workspace limits, -1 if none */
+  int64_t first_err;      /* lowest index whose solve raised, -1 if none */
+  int32_t first_err_code; /* ik_status of first_err */
+  int32_t max_iters;      /* FABRIK: max iterations over the batch */
+  int64_t sum_iters;      /* FABRIK: total iterations */
+  int64_t n_capped;       /* FABRIK: points that hit max_iter */
+  double max_fk_err;      /* ANN: max |FK(theta) - p|_2 over the batch (if requested) */
+  double sum_fk_err;      /* ANN: sum of |FK(theta) - p|_2 */
+} ik_stats;
+
+/* ---- context ----------------------------------------------------------- */
+/* One context per device; owns a stream, device scratch and model weights. */
+int ik_ctx_create(int device, ik_ctx **out);
+int ik_ctx_destroy(ik_ctx *ctx);
+/* Use an external stream (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int ik_ctx_set_stream(ik_ctx *ctx, void *stream);
+void *ik_ctx_get_stream(ik_ctx *ctx);
+const char *ik_last_error(void); /* thread-local message of the last failure */
+const char *ik_version(void);
+
+/* ---- robot ---------------------------------------------------------------
+ * robot/robot.py:38-42 SixDOFRobot: dh is the 4x4 row-major DH matrix
+ * (rows thetas, d, a, alpha), links the 4 joint distances, limits
+ * {x_lo, x_hi, y_lo, y_hi, z_lo, z_hi} (inclusive).  Defaults are SixDOFRobot's. */
+int ik_set_robot(ik_ctx *ctx, const double *dh, const double *links, const double *limits);
+
+/* ---- workspace check ----------------------------------------------------
+ * InverseKinematics.check_limits, kinematics/inverse.py:26-35. */
+int ik_check_limits(ik_ctx *ctx, const double *pts, int64_t n, int flags, ik_stats *stats);
+
+/* ---- forward kinematics --------------------------------------------------
+ * ForwardKinematics.fkine, kinematics/forward.py:73-94, batched: ang n x 4
+ * (float64) -> effector xyz n x 3 and, if mats is not NULL, the four
+ * cumulative transforms M_1..M_4 (n x 4 x 4 x 4, row-major; fkine's second
+ * return value).  Angles outside [-2pi, 2pi] give IK_E_ANGLE_RANGE in stats. */
+int ik_fk(ik_ctx *ctx, const double *ang, int64_t n, double *xyz, double *mats, int flags,
+          ik_stats *stats);
+
+/* ---- FABRIK ---------------------------------------------------------------
+ * FabrikInverseKinematics.ikine, kinematics/inverse.py:115-139 (+ check_limits,
+ * Fabrik.calculate fabrik.py:44-67, __get_angles inverse.py:54-112), batched:
+ * pts n x 3 -> ang n x 4 (float64), iters n (nullable), final joint positions
+ * n x 4 x 3 (nullable).  tol/max_iter: Fabrik(err_margin, max_iter_num). */
+int ik_fabrik_solve(ik_ctx *ctx, const double *pts, int64_t n, double tol, int32_t max_iter,
+                    double *ang, int32_t *iters, double *joints, int flags, ik_stats *stats);
+
+/* Fabrik.calculate, kinematics/fabrik.py:44-67, batched over n goals for a chain
+ * of nj (2..8) joints: init is n x nj x 3 (or nj x 3 shared by all goals when
+ * init_shared != 0), goals n x 3 -> joints n x nj x 3, iters n (nullable). */
+int ik_fabrik_calc(ik_ctx *ctx, int nj, const double *dists, const double *init,
+                   int init_shared, const double *goals, int64_t n, double tol,
+                   int32_t max_iter, double *joints, int32_t *iters, int flags,
+                   ik_stats *stats);
+
+/* ---- ANN ----------------------------------------------------------------
+ * ANN.load_model, kinematics/ann.py:78-85, with the decoded model: n_layers
+ * Dense layers, dims[0..n_layers] (dims[0] == 3, dims[n_layers] == 4), acts[l]
+ * one of IK_ACT_*, W[l] host float32 [dims[l]][dims[l+1]] row-major (the Keras
+ * kernel layout, x @ W + b), b[l] host float32 [dims[l+1]], and the two
+ * StandardScalers (ann.py:83-84).  Widths up to 512. */
+int ik_ann_load(ik_ctx *ctx, int n_layers, const int32_t *dims, const int32_t *acts,
+                const float *const *W, const float *const *b, const double *x_mean,
+                const double *x_scale, const double *y_mean, const double *y_scale);
+
+/* ANN.predict, kinematics/ann.py:70-76 (+ check_limits for AnnInverseKinematics.ikine,
+ * inverse.py:152-155 unless IK_F_NO_LIMITS): pts n x 3 float64 -> ang n x 4
+ * float32.  fk_err (nullable) n float64: |FK(ang) - p|_2, the cli.py:54-61
+ * round trip, fused into the same launch; its max/sum go to stats. */
+int ik_ann_solve(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *fk_err,
+                 int flags, ik_stats *stats);
+
+/* Per-kernel timing with HIP events on the context's stream: when on, every
+ * kernel a call launches is bracketed by hipEventRecord.  ik_kernel_times
+ * waits for the last call's events and returns how many kernels it timed,
+ * their durations in ms and (if names != NULL) their names, name_len bytes
+ * each; a negative value is -ik_status. */
+int ik_ctx_set_timing(ik_ctx *ctx, int on);
+int ik_kernel_times(ik_ctx *ctx, int max, float *ms, char *names, int name_len);
+
+/* After IK_F_ASYNC calls: wait for the stream and read the accumulated stats
+ * of the last call. */
+int ik_stats_fetch(ik_ctx *ctx, ik_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IKHIP_H */

@@ -1,0 +1,299 @@
+"""ctypes binding of libikhip.so (the C ABI in include/ikhip.h).
+
+The product path has no CPU fallback: if the shared library is missing or no
+HIP device can be opened, every solve raises (NativeUnavailable).  Arrays may be
+numpy host arrays (staged by the library) or torch CUDA tensors on the
+context's device (passed as device pointers, computed in place on the
+context's stream).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+import threading
+from typing import Optional, Sequence
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libikhip.so")
+
+IK_OK, IK_E_OUT_OF_REACH, IK_E_DOMAIN, IK_E_ZERODIV, IK_E_ANGLE_RANGE = 0, 1, 2, 3, 4
+IK_E_BADARG, IK_E_HIP, IK_E_NOMODEL = 16, 17, 18
+IK_F_DEVICE, IK_F_ASYNC, IK_F_NO_LIMITS = 1, 2, 4
+ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
+
+EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_ctx_get_stream",
+                    "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk",
+                    "ik_fabrik_solve", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
+                    "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times")
+
+
+class NativeUnavailable(RuntimeError):
+    """libikhip.so is not built or no gfx950 device is usable."""
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libikhip error {code}: {msg}")
+        self.code = code
+
+
+class IkStats(ctypes.Structure):
+    _fields_ = [("first_oob", ctypes.c_int64), ("first_err", ctypes.c_int64),
+                ("first_err_code", ctypes.c_int32), ("max_iters", ctypes.c_int32),
+                ("sum_iters", ctypes.c_int64), ("n_capped", ctypes.c_int64),
+                ("max_fk_err", ctypes.c_double), ("sum_fk_err", ctypes.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libikhip.so.  torch (if installed) is imported first so that the
+    process has exactly one HIP runtime (torch ships its own libamdhip64)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NativeUnavailable(
+                f"{path} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(or `make -C inversekinematicsann_amd/csrc`)")
+        if "torch" not in sys.modules:
+            try:
+                import torch  # noqa: F401
+            except Exception:  # noqa: BLE001 -- torch is optional plumbing
+                pass
+        L = ctypes.CDLL(path)
+        vp, dp, ip = ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p
+        i64, i32 = ctypes.c_int64, ctypes.c_int32
+        st = ctypes.POINTER(IkStats)
+        L.ik_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.ik_ctx_destroy.argtypes = [vp]
+        L.ik_ctx_set_stream.argtypes = [vp, vp]
+        L.ik_ctx_get_stream.argtypes = [vp]
+        L.ik_ctx_get_stream.restype = vp
+        L.ik_last_error.restype = ctypes.c_char_p
+        L.ik_version.restype = ctypes.c_char_p
+        L.ik_set_robot.argtypes = [vp, dp, dp, dp]
+        L.ik_check_limits.argtypes = [vp, dp, i64, ctypes.c_int, st]
+        L.ik_fk.argtypes = [vp, dp, i64, dp, dp, ctypes.c_int, st]
+        L.ik_fabrik_solve.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp, ctypes.c_int,
+                                      st]
+        L.ik_fabrik_calc.argtypes = [vp, ctypes.c_int, dp, dp, ctypes.c_int, dp, i64,
+                                     ctypes.c_double, i32, dp, ip, ctypes.c_int, st]
+        L.ik_ann_load.argtypes = [vp, ctypes.c_int, ip, ip, ctypes.POINTER(ctypes.c_void_p),
+                                  ctypes.POINTER(ctypes.c_void_p), dp, dp, dp, dp]
+        L.ik_ann_solve.argtypes = [vp, dp, i64, dp, dp, ctypes.c_int, st]
+        L.ik_stats_fetch.argtypes = [vp, st]
+        L.ik_ctx_set_timing.argtypes = [vp, ctypes.c_int]
+        L.ik_kernel_times.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int]
+        _lib = L
+        return L
+
+
+def _ptr(a) -> Optional[int]:
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def _is_device(a) -> bool:
+    return hasattr(a, "is_cuda") and bool(a.is_cuda)
+
+
+def _host(a, dtype, shape_last=None):
+    arr = np.ascontiguousarray(a, dtype=dtype)
+    if shape_last is not None:
+        arr = arr.reshape(-1, shape_last)
+    return arr
+
+
+class Context:
+    """One libikhip context (device, stream, scratch, ANN weights)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.ik_ctx_create(int(device), ctypes.byref(h))
+        if rc != IK_OK:
+            raise NativeUnavailable(f"ik_ctx_create(device={device}) failed: "
+                                    f"{self.lib.ik_last_error().decode()}")
+        self.handle = h
+        self.device = int(device)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.ik_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def _check(self, rc: int):
+        if rc != IK_OK:
+            raise NativeError(rc, self.lib.ik_last_error().decode())
+
+    # -- configuration ------------------------------------------------------
+    def set_stream(self, stream_handle: Optional[int]):
+        self._check(self.lib.ik_ctx_set_stream(self.handle, stream_handle))
+
+    def set_robot(self, dh, links, limits):
+        dh = _host(dh, np.float64).reshape(16)
+        links = _host(links, np.float64).reshape(4)
+        limits = _host(limits, np.float64).reshape(6)
+        self._check(self.lib.ik_set_robot(self.handle, _ptr(dh), _ptr(links), _ptr(limits)))
+
+    # -- solves ---------------------------------------------------------------
+    def check_limits(self, pts) -> IkStats:
+        s = IkStats()
+        if _is_device(pts):
+            self._check(self.lib.ik_check_limits(self.handle, _ptr(pts), pts.shape[0],
+                                                 IK_F_DEVICE, ctypes.byref(s)))
+        else:
+            p = _host(pts, np.float64, 3)
+            self._check(self.lib.ik_check_limits(self.handle, _ptr(p), p.shape[0], 0,
+                                                 ctypes.byref(s)))
+        return s
+
+    def fk(self, ang, with_mats: bool = False):
+        """Batched FK: returns (xyz n x 3, mats n x 4 x 4 x 4 or None, stats)."""
+        s = IkStats()
+        a = _host(ang, np.float64, 4)
+        n = a.shape[0]
+        xyz = np.empty((n, 3), np.float64)
+        mats = np.empty((n, 4, 4, 4), np.float64) if with_mats else None
+        self._check(self.lib.ik_fk(self.handle, _ptr(a), n, _ptr(xyz), _ptr(mats), 0,
+                                   ctypes.byref(s)))
+        return xyz, mats, s
+
+    def fk_device(self, ang, xyz, flags: int = IK_F_DEVICE):
+        s = IkStats()
+        self._check(self.lib.ik_fk(self.handle, _ptr(ang), ang.shape[0], _ptr(xyz), None,
+                                   flags, ctypes.byref(s)))
+        return s
+
+    def fabrik_solve(self, pts, tol=1e-3, max_iter=100, check_limits=True,
+                     want_iters=True, want_joints=False):
+        """Host arrays in/out: returns (angles n x 4 f64, iters, joints, stats)."""
+        s = IkStats()
+        p = _host(pts, np.float64, 3)
+        n = p.shape[0]
+        ang = np.empty((n, 4), np.float64)
+        it = np.empty(n, np.int32) if want_iters else None
+        jo = np.empty((n, 4, 3), np.float64) if want_joints else None
+        flags = 0 if check_limits else IK_F_NO_LIMITS
+        self._check(self.lib.ik_fabrik_solve(self.handle, _ptr(p), n, float(tol), int(max_iter),
+                                             _ptr(ang), _ptr(it), _ptr(jo), flags,
+                                             ctypes.byref(s)))
+        return ang, it, jo, s
+
+    def fabrik_solve_device(self, pts, ang, iters=None, joints=None, tol=1e-3, max_iter=100,
+                            flags: int = IK_F_DEVICE):
+        s = IkStats()
+        self._check(self.lib.ik_fabrik_solve(self.handle, _ptr(pts), pts.shape[0], float(tol),
+                                             int(max_iter), _ptr(ang), _ptr(iters),
+                                             _ptr(joints), flags, ctypes.byref(s)))
+        return s
+
+    def fabrik_calc(self, dists, init, goals, tol=1e-3, max_iter=100):
+        """Batched Fabrik.calculate; init n x nj x 3 or nj x 3 (shared)."""
+        s = IkStats()
+        d = _host(dists, np.float64).reshape(-1)
+        nj = d.shape[0]
+        ini = np.ascontiguousarray(init, dtype=np.float64)
+        shared = 1 if ini.ndim == 2 else 0
+        g = _host(goals, np.float64, 3)
+        n = g.shape[0]
+        if ini.shape[-2:] != (nj, 3) or (not shared and ini.shape[0] != n):
+            raise ValueError("init must be n x nj x 3 or nj x 3")
+        out = np.empty((n, nj, 3), np.float64)
+        it = np.empty(n, np.int32)
+        self._check(self.lib.ik_fabrik_calc(self.handle, nj, _ptr(d), _ptr(ini), shared, _ptr(g),
+                                            n, float(tol), int(max_iter), _ptr(out), _ptr(it),
+                                            0, ctypes.byref(s)))
+        return out, it, s
+
+    def ann_load(self, weights: Sequence, biases: Sequence, acts: Sequence[str], x_mean,
+                 x_scale, y_mean, y_scale):
+        Ws = [np.ascontiguousarray(w, dtype=np.float32) for w in weights]
+        bs = [np.ascontiguousarray(b, dtype=np.float32).reshape(-1) for b in biases]
+        nl = len(Ws)
+        dims = [Ws[0].shape[0]] + [w.shape[1] for w in Ws]
+        for l in range(nl):
+            if Ws[l].shape != (dims[l], dims[l + 1]) or bs[l].shape != (dims[l + 1],):
+                raise ValueError(f"layer {l}: kernel {Ws[l].shape} / bias {bs[l].shape} mismatch")
+        dims_a = np.array(dims, np.int32)
+        acts_a = np.array([ACTS[a] for a in acts], np.int32)
+        wp = (ctypes.c_void_p * nl)(*[w.ctypes.data for w in Ws])
+        bp = (ctypes.c_void_p * nl)(*[b.ctypes.data for b in bs])
+        sc = [_host(v, np.float64).reshape(-1) for v in (x_mean, x_scale, y_mean, y_scale)]
+        self._check(self.lib.ik_ann_load(self.handle, nl, _ptr(dims_a), _ptr(acts_a), wp, bp,
+                                         *[_ptr(v) for v in sc]))
+
+    def ann_solve(self, pts, check_limits=True, want_fk_err=False):
+        s = IkStats()
+        p = _host(pts, np.float64, 3)
+        n = p.shape[0]
+        ang = np.empty((n, 4), np.float32)
+        err = np.empty(n, np.float64) if want_fk_err else None
+        flags = 0 if check_limits else IK_F_NO_LIMITS
+        self._check(self.lib.ik_ann_solve(self.handle, _ptr(p), n, _ptr(ang), _ptr(err), flags,
+                                          ctypes.byref(s)))
+        return ang, err, s
+
+    def ann_solve_device(self, pts, ang, fk_err=None, flags: int = IK_F_DEVICE):
+        s = IkStats()
+        self._check(self.lib.ik_ann_solve(self.handle, _ptr(pts), pts.shape[0], _ptr(ang),
+                                          _ptr(fk_err), flags, ctypes.byref(s)))
+        return s
+
+    def set_timing(self, on: bool = True):
+        self._check(self.lib.ik_ctx_set_timing(self.handle, 1 if on else 0))
+
+    def kernel_times(self):
+        """[(kernel name, ms)] of the last call (after set_timing(True))."""
+        ms = np.zeros(16, np.float32)
+        names = ctypes.create_string_buffer(16 * 48)
+        n = self.lib.ik_kernel_times(self.handle, 16, ms.ctypes.data, ctypes.addressof(names), 48)
+        if n < 0:
+            raise NativeError(-n, self.lib.ik_last_error().decode())
+        raw = names.raw
+        return [(raw[i * 48:(i + 1) * 48].split(b"\0")[0].decode(), float(ms[i]))
+                for i in range(n)]
+
+    def stats_fetch(self) -> IkStats:
+        s = IkStats()
+        self._check(self.lib.ik_stats_fetch(self.handle, ctypes.byref(s)))
+        return s
+
+
+_default_ctx: Optional[Context] = None
+_default_lock = threading.Lock()
+
+
+def default_device() -> int:
+    for k in ("IKHIP_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(k):
+            return int(os.environ[k])
+    return 0
+
+
+def context() -> Context:
+    """The process-wide context on default_device()."""
+    global _default_ctx
+    with _default_lock:
+        if _default_ctx is None:
+            _default_ctx = Context(default_device())
+        return _default_ctx

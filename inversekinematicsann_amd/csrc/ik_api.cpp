@@ -1,0 +1,512 @@
+// ik_api.cpp -- the C ABI of libikhip.so (declared in include/ikhip.h).
+//
+// Owns per-context state: the HIP stream, the device-side stats block, a
+// grow-only device scratch buffer (host-pointer calls stage through it), the
+// robot constants and the packed ANN weights.  No allocation happens inside a
+// solve call once the scratch is large enough, so IK_F_DEVICE|IK_F_ASYNC calls
+// can be captured in a hipGraph.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ik_common.h"
+
+using namespace ikhip;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define IK_HIP(call)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return fail(IK_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
+  } while (0)
+
+const double kDefaultDh[16] = {0.0, kPi / 2, 0.0, 0.0, 2.0, 0.0, 0.0, 0.0,
+                               0.0, 2.0,     2.0, 2.0, kPi / 2, 0.0, 0.0, 0.0};
+const double kDefaultLinks[4] = {2.0, 2.0, 2.0, 2.0};
+const double kDefaultLimits[6] = {0.0, 6.0, -6.0, 6.0, -3.0, 6.0};
+
+constexpr int kMaxTimed = 16;
+struct KTimer {
+  bool on = false;
+  int n = 0;
+  hipEvent_t beg[kMaxTimed] = {};
+  hipEvent_t end[kMaxTimed] = {};
+  const char *name[kMaxTimed] = {};
+};
+thread_local KTimer *g_kt = nullptr;
+
+}  // namespace
+
+namespace ikhip {
+void kt_begin(const char *name, hipStream_t st) {
+  if (!g_kt || !g_kt->on || g_kt->n >= kMaxTimed) return;
+  g_kt->name[g_kt->n] = name;
+  (void)hipEventRecord(g_kt->beg[g_kt->n], st);
+}
+void kt_end(hipStream_t st) {
+  if (!g_kt || !g_kt->on || g_kt->n >= kMaxTimed) return;
+  (void)hipEventRecord(g_kt->end[g_kt->n], st);
+  g_kt->n++;
+}
+}  // namespace ikhip
+
+struct ik_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  DevStats *d_stats = nullptr;
+  DevStats *h_stats = nullptr;  // pinned
+  void *scratch = nullptr;
+  size_t scratch_bytes = 0;
+  RobotDev robot;
+  bool ann_loaded = false;
+  AnnModelDev ann;
+  void *ann_buf = nullptr;
+  int fabrik_variant = 1;
+  KTimer kt;
+};
+
+namespace {
+
+struct KtScope {
+  explicit KtScope(ik_ctx *c) {
+    g_kt = &c->kt;
+    c->kt.n = 0;
+  }
+  ~KtScope() { g_kt = nullptr; }
+};
+
+int ensure_scratch(ik_ctx *c, size_t bytes) {
+  if (bytes <= c->scratch_bytes) return IK_OK;
+  IK_HIP(hipStreamSynchronize(c->stream));
+  if (c->scratch) IK_HIP(hipFree(c->scratch));
+  c->scratch = nullptr;
+  c->scratch_bytes = 0;
+  size_t want = bytes + bytes / 4 + (1 << 20);
+  IK_HIP(hipMalloc(&c->scratch, want));
+  c->scratch_bytes = want;
+  return IK_OK;
+}
+
+int set_dev(ik_ctx *c) {
+  IK_HIP(hipSetDevice(c->device));
+  return IK_OK;
+}
+
+void stats_from_dev(const DevStats &d, ik_stats *s) {
+  s->first_oob = (d.first_oob == ~0ull) ? -1 : (int64_t)d.first_oob;
+  if (d.first_err_key == ~0ull) {
+    s->first_err = -1;
+    s->first_err_code = IK_OK;
+  } else {
+    s->first_err = (int64_t)(d.first_err_key >> 8);
+    s->first_err_code = (int32_t)(d.first_err_key & 0xff);
+  }
+  s->max_iters = d.max_iters;
+  s->sum_iters = (int64_t)d.sum_iters;
+  s->n_capped = (int64_t)d.n_capped;
+  double mx;
+  std::memcpy(&mx, &d.max_fk_err_bits, sizeof(mx));
+  s->max_fk_err = mx;
+  s->sum_fk_err = d.sum_fk_err;
+}
+
+int finish(ik_ctx *c, int flags, ik_stats *stats) {
+  if (flags & IK_F_ASYNC) return IK_OK;
+  IK_HIP(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(DevStats), hipMemcpyDeviceToHost,
+                        c->stream));
+  IK_HIP(hipStreamSynchronize(c->stream));
+  if (stats) stats_from_dev(*c->h_stats, stats);
+  return IK_OK;
+}
+
+// Staging plan for host-pointer calls: inputs copied into scratch, outputs
+// produced in scratch and copied back.
+struct Stage {
+  ik_ctx *c;
+  bool dev;
+  size_t off = 0;
+  char *base = nullptr;
+  struct Out {
+    void *host;
+    void *devp;
+    size_t bytes;
+  };
+  std::vector<Out> outs;
+  Stage(ik_ctx *cc, bool d) : c(cc), dev(d) {}
+  static size_t up(size_t b) { return (b + 255) & ~(size_t)255; }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char *ik_last_error(void) { return g_last_error.c_str(); }
+const char *ik_version(void) { return "ikhip 0.1 gfx950"; }
+
+int ik_ctx_create(int device, ik_ctx **out) {
+  if (!out) return fail(IK_E_BADARG, "ik_ctx_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  IK_HIP(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev)
+    return fail(IK_E_BADARG, "ik_ctx_create: device " + std::to_string(device) +
+                                 " out of range (" + std::to_string(ndev) + " devices)");
+  ik_ctx *c = new ik_ctx();
+  c->device = device;
+  int rc = set_dev(c);
+  if (rc) {
+    delete c;
+    return rc;
+  }
+  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc(&c->d_stats, sizeof(DevStats));
+  if (e == hipSuccess) e = hipHostMalloc(&c->h_stats, sizeof(DevStats), hipHostMallocDefault);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(IK_E_HIP, std::string("ik_ctx_create: ") + hipGetErrorString(e));
+  }
+  c->stream = c->own_stream;
+  std::memcpy(c->robot.dh, kDefaultDh, sizeof(kDefaultDh));
+  std::memcpy(c->robot.links, kDefaultLinks, sizeof(kDefaultLinks));
+  std::memcpy(c->robot.lim, kDefaultLimits, sizeof(kDefaultLimits));
+  if (const char *v = std::getenv("IKHIP_FABRIK_VARIANT")) c->fabrik_variant = std::atoi(v);
+  *out = c;
+  return IK_OK;
+}
+
+int ik_ctx_destroy(ik_ctx *c) {
+  if (!c) return IK_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->ann_buf) (void)hipFree(c->ann_buf);
+  if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->h_stats) (void)hipHostFree(c->h_stats);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  for (int i = 0; i < kMaxTimed; ++i) {
+    if (c->kt.beg[i]) (void)hipEventDestroy(c->kt.beg[i]);
+    if (c->kt.end[i]) (void)hipEventDestroy(c->kt.end[i]);
+  }
+  delete c;
+  return IK_OK;
+}
+
+int ik_ctx_set_stream(ik_ctx *c, void *stream) {
+  if (!c) return fail(IK_E_BADARG, "ik_ctx_set_stream: NULL context");
+  c->stream = stream ? static_cast<hipStream_t>(stream) : c->own_stream;
+  return IK_OK;
+}
+
+void *ik_ctx_get_stream(ik_ctx *c) { return c ? static_cast<void *>(c->stream) : nullptr; }
+
+int ik_set_robot(ik_ctx *c, const double *dh, const double *links, const double *limits) {
+  if (!c) return fail(IK_E_BADARG, "ik_set_robot: NULL context");
+  if (dh) std::memcpy(c->robot.dh, dh, sizeof(c->robot.dh));
+  if (links) std::memcpy(c->robot.links, links, sizeof(c->robot.links));
+  if (limits) std::memcpy(c->robot.lim, limits, sizeof(c->robot.lim));
+  return IK_OK;
+}
+
+int ik_ctx_set_timing(ik_ctx *c, int on) {
+  if (!c) return fail(IK_E_BADARG, "ik_ctx_set_timing: NULL context");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  if (on && !c->kt.beg[0]) {
+    for (int i = 0; i < kMaxTimed; ++i) {
+      IK_HIP(hipEventCreate(&c->kt.beg[i]));
+      IK_HIP(hipEventCreate(&c->kt.end[i]));
+    }
+  }
+  c->kt.on = on != 0;
+  c->kt.n = 0;
+  return IK_OK;
+}
+
+int ik_kernel_times(ik_ctx *c, int max, float *ms, char *names, int name_len) {
+  if (!c || max < 0 || (max > 0 && !ms)) return -IK_E_BADARG;
+  if (!c->kt.on) return 0;
+  if (set_dev(c)) return -IK_E_HIP;
+  int n = c->kt.n < max ? c->kt.n : max;
+  for (int i = 0; i < n; ++i) {
+    if (hipEventSynchronize(c->kt.end[i]) != hipSuccess) return -IK_E_HIP;
+    float t = 0.0f;
+    if (hipEventElapsedTime(&t, c->kt.beg[i], c->kt.end[i]) != hipSuccess) return -IK_E_HIP;
+    ms[i] = t;
+    if (names && name_len > 0) {
+      std::strncpy(names + (size_t)i * name_len, c->kt.name[i], (size_t)name_len - 1);
+      names[(size_t)i * name_len + name_len - 1] = 0;
+    }
+  }
+  return n;
+}
+
+int ik_stats_fetch(ik_ctx *c, ik_stats *stats) {
+  if (!c) return fail(IK_E_BADARG, "ik_stats_fetch: NULL context");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  return finish(c, 0, stats);
+}
+
+int ik_check_limits(ik_ctx *c, const double *pts, int64_t n, int flags, ik_stats *stats) {
+  if (!c || n < 0 || (n > 0 && !pts)) return fail(IK_E_BADARG, "ik_check_limits: bad args");
+  if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
+    return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);
+  const double *dp = pts;
+  if (!(flags & IK_F_DEVICE)) {
+    if ((rc = ensure_scratch(c, (size_t)n * 24 + 256))) return rc;
+    IK_HIP(hipMemcpyAsync(c->scratch, pts, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    dp = static_cast<const double *>(c->scratch);
+  }
+  launch_reset_stats(c->d_stats, c->stream);
+  launch_check_limits(c->robot, dp, n, c->d_stats, c->stream);
+  IK_HIP(hipGetLastError());
+  return finish(c, flags, stats);
+}
+
+int ik_fk(ik_ctx *c, const double *ang, int64_t n, double *xyz, double *mats, int flags,
+          ik_stats *stats) {
+  double *joints = mats;  // n x 4 x 16
+  if (!c || n < 0 || (n > 0 && (!ang || !xyz))) return fail(IK_E_BADARG, "ik_fk: bad args");
+  if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
+    return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);
+  const double *da = ang;
+  double *dx = xyz, *dj = joints;
+  if (!(flags & IK_F_DEVICE)) {
+    size_t b_in = Stage::up((size_t)n * 32), b_x = Stage::up((size_t)n * 24),
+           b_j = joints ? Stage::up((size_t)n * 512) : 0;
+    if ((rc = ensure_scratch(c, b_in + b_x + b_j))) return rc;
+    char *s = static_cast<char *>(c->scratch);
+    IK_HIP(hipMemcpyAsync(s, ang, (size_t)n * 32, hipMemcpyHostToDevice, c->stream));
+    da = reinterpret_cast<double *>(s);
+    dx = reinterpret_cast<double *>(s + b_in);
+    dj = joints ? reinterpret_cast<double *>(s + b_in + b_x) : nullptr;
+  }
+  launch_reset_stats(c->d_stats, c->stream);
+  launch_fk(c->robot, da, n, dx, dj, c->d_stats, c->stream);
+  IK_HIP(hipGetLastError());
+  if (!(flags & IK_F_DEVICE) && n > 0) {
+    IK_HIP(hipMemcpyAsync(xyz, dx, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    if (joints)
+      IK_HIP(hipMemcpyAsync(joints, dj, (size_t)n * 512, hipMemcpyDeviceToHost, c->stream));
+  }
+  return finish(c, flags, stats);
+}
+
+int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t max_iter,
+                    double *ang, int32_t *iters, double *joints, int flags, ik_stats *stats) {
+  if (!c || n < 0 || (n > 0 && (!pts || !ang)) || max_iter < 0)
+    return fail(IK_E_BADARG, "ik_fabrik_solve: bad args");
+  if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
+    return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);
+  const bool dev = flags & IK_F_DEVICE;
+  size_t b_work = Stage::up(fabrik_scratch_bytes(n));
+  size_t b_in = dev ? 0 : Stage::up((size_t)n * 24);
+  size_t b_ang = dev ? 0 : Stage::up((size_t)n * 32);
+  size_t b_it = (dev || !iters) ? 0 : Stage::up((size_t)n * 4);
+  size_t b_jo = (dev || !joints) ? 0 : Stage::up((size_t)n * 96);
+  if ((rc = ensure_scratch(c, b_work + b_in + b_ang + b_it + b_jo))) return rc;
+  char *s = static_cast<char *>(c->scratch);
+  void *work = s;
+  const double *dp = pts;
+  double *da = ang, *dj = joints;
+  int32_t *di = iters;
+  if (!dev) {
+    char *q = s + b_work;
+    dp = reinterpret_cast<double *>(q);
+    IK_HIP(hipMemcpyAsync(q, pts, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    q += b_in;
+    da = reinterpret_cast<double *>(q);
+    q += b_ang;
+    di = iters ? reinterpret_cast<int32_t *>(q) : nullptr;
+    q += b_it;
+    dj = joints ? reinterpret_cast<double *>(q) : nullptr;
+  }
+  launch_reset_stats(c->d_stats, c->stream);
+  launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj,
+                      !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
+                      c->fabrik_variant);
+  IK_HIP(hipGetLastError());
+  if (!dev && n > 0) {
+    IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
+    if (iters)
+      IK_HIP(hipMemcpyAsync(iters, di, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+    if (joints)
+      IK_HIP(hipMemcpyAsync(joints, dj, (size_t)n * 96, hipMemcpyDeviceToHost, c->stream));
+  }
+  return finish(c, flags, stats);
+}
+
+int ik_fabrik_calc(ik_ctx *c, int nj, const double *dists, const double *init,
+                   int init_shared, const double *goals, int64_t n, double tol,
+                   int32_t max_iter, double *joints, int32_t *iters, int flags,
+                   ik_stats *stats) {
+  if (!c || nj < 2 || nj > 8 || !dists || n < 0 || (n > 0 && (!init || !goals || !joints)) ||
+      max_iter < 0)
+    return fail(IK_E_BADARG, "ik_fabrik_calc: bad args (nj must be 2..8)");
+  if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
+    return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);
+  const bool dev = flags & IK_F_DEVICE;
+  size_t b_d = Stage::up((size_t)nj * 8);
+  size_t n_init = init_shared ? (size_t)nj * 3 : (size_t)n * nj * 3;
+  size_t b_init = dev ? 0 : Stage::up(n_init * 8);
+  size_t b_g = dev ? 0 : Stage::up((size_t)n * 24);
+  size_t b_jo = dev ? 0 : Stage::up((size_t)n * nj * 24);
+  size_t b_it = (dev || !iters) ? 0 : Stage::up((size_t)n * 4);
+  if ((rc = ensure_scratch(c, b_d + b_init + b_g + b_jo + b_it))) return rc;
+  char *s = static_cast<char *>(c->scratch);
+  // the link distances always travel from host memory
+  IK_HIP(hipMemcpyAsync(s, dists, (size_t)nj * 8, hipMemcpyHostToDevice, c->stream));
+  const double *dd = reinterpret_cast<double *>(s);
+  const double *di = init, *dg = goals;
+  double *djo = joints;
+  int32_t *dit = iters;
+  if (!dev) {
+    char *q = s + b_d;
+    IK_HIP(hipMemcpyAsync(q, init, n_init * 8, hipMemcpyHostToDevice, c->stream));
+    di = reinterpret_cast<double *>(q);
+    q += b_init;
+    IK_HIP(hipMemcpyAsync(q, goals, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    dg = reinterpret_cast<double *>(q);
+    q += b_g;
+    djo = reinterpret_cast<double *>(q);
+    q += b_jo;
+    dit = iters ? reinterpret_cast<int32_t *>(q) : nullptr;
+  }
+  launch_reset_stats(c->d_stats, c->stream);
+  launch_fabrik_calc(nj, dd, di, init_shared != 0, dg, n, tol, max_iter, djo, dit, c->d_stats,
+                     c->stream);
+  IK_HIP(hipGetLastError());
+  if (!dev && n > 0) {
+    IK_HIP(hipMemcpyAsync(joints, djo, (size_t)n * nj * 24, hipMemcpyDeviceToHost, c->stream));
+    if (iters)
+      IK_HIP(hipMemcpyAsync(iters, dit, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
+  }
+  // dists came from a host buffer that may go away: always complete before return
+  if (flags & IK_F_ASYNC) IK_HIP(hipStreamSynchronize(c->stream));
+  return finish(c, flags, stats);
+}
+
+int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *acts,
+                const float *const *W, const float *const *b, const double *x_mean,
+                const double *x_scale, const double *y_mean, const double *y_scale) {
+  if (!c || n_layers < 1 || n_layers > kAnnMaxLayers || !dims || !acts || !W || !b ||
+      !x_mean || !x_scale || !y_mean || !y_scale)
+    return fail(IK_E_BADARG, "ik_ann_load: bad args");
+  if (dims[0] != 3 || dims[n_layers] != 4)
+    return fail(IK_E_BADARG, "ik_ann_load: the model must map 3 inputs to 4 outputs");
+  for (int l = 0; l <= n_layers; ++l)
+    if (dims[l] < 1 || dims[l] > kAnnMaxWidth)
+      return fail(IK_E_BADARG, "ik_ann_load: layer widths must be 1.." +
+                                   std::to_string(kAnnMaxWidth));
+  for (int l = 0; l < n_layers; ++l)
+    if (acts[l] < IK_ACT_LINEAR || acts[l] > IK_ACT_SIGMOID)
+      return fail(IK_E_BADARG, "ik_ann_load: unsupported activation code");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  // one device buffer: per layer packed weights then padded bias
+  std::vector<size_t> woff(n_layers), boff(n_layers);
+  size_t total = 0;
+  for (int l = 0; l < n_layers; ++l) {
+    woff[l] = total;
+    total += ann_packed_floats(dims[l], dims[l + 1]) * 4;
+    total = (total + 255) & ~(size_t)255;
+    boff[l] = total;
+    total += (size_t)((dims[l + 1] + 31) / 32 * 32) * 4;
+    total = (total + 255) & ~(size_t)255;
+  }
+  std::vector<char> host(total, 0);
+  for (int l = 0; l < n_layers; ++l) {
+    ann_pack_layer(W[l], dims[l], dims[l + 1], reinterpret_cast<float *>(&host[woff[l]]));
+    std::memcpy(&host[boff[l]], b[l], (size_t)dims[l + 1] * 4);
+  }
+  IK_HIP(hipStreamSynchronize(c->stream));
+  if (c->ann_buf) IK_HIP(hipFree(c->ann_buf));
+  c->ann_buf = nullptr;
+  c->ann_loaded = false;
+  IK_HIP(hipMalloc(&c->ann_buf, total));
+  IK_HIP(hipMemcpy(c->ann_buf, host.data(), total, hipMemcpyHostToDevice));
+  AnnModelDev &m = c->ann;
+  std::memset(&m, 0, sizeof(m));
+  m.n_layers = n_layers;
+  char *base = static_cast<char *>(c->ann_buf);
+  for (int l = 0; l < n_layers; ++l) {
+    m.kp[l] = (dims[l] + 7) / 8 * 8;
+    m.np[l] = (dims[l + 1] + 31) / 32 * 32;
+    m.act[l] = acts[l];
+    m.wp[l] = reinterpret_cast<const float4 *>(base + woff[l]);
+    m.bias[l] = reinterpret_cast<const float *>(base + boff[l]);
+  }
+  for (int i = 0; i < 3; ++i) {
+    m.xm[i] = x_mean[i];
+    m.xs[i] = x_scale[i];
+  }
+  for (int i = 0; i < 4; ++i) {
+    m.ym[i] = y_mean[i];
+    m.ys[i] = y_scale[i];
+  }
+  c->ann_loaded = true;
+  return IK_OK;
+}
+
+int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk_err,
+                 int flags, ik_stats *stats) {
+  if (!c || n < 0 || (n > 0 && (!pts || !ang))) return fail(IK_E_BADARG, "ik_ann_solve: bad args");
+  if (!c->ann_loaded) return fail(IK_E_NOMODEL, "ik_ann_solve: no model loaded (ik_ann_load)");
+  if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
+    return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);
+  const bool dev = flags & IK_F_DEVICE;
+  const double *dp = pts;
+  float *da = ang;
+  double *de = fk_err;
+  if (!dev) {
+    size_t b_in = Stage::up((size_t)n * 24), b_a = Stage::up((size_t)n * 16),
+           b_e = fk_err ? Stage::up((size_t)n * 8) : 0;
+    if ((rc = ensure_scratch(c, b_in + b_a + b_e))) return rc;
+    char *s = static_cast<char *>(c->scratch);
+    IK_HIP(hipMemcpyAsync(s, pts, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    dp = reinterpret_cast<double *>(s);
+    da = reinterpret_cast<float *>(s + b_in);
+    de = fk_err ? reinterpret_cast<double *>(s + b_in + b_a) : nullptr;
+  }
+  launch_reset_stats(c->d_stats, c->stream);
+  launch_ann(c->ann, c->robot, dp, n, da, de, !(flags & IK_F_NO_LIMITS), c->d_stats, c->stream);
+  IK_HIP(hipGetLastError());
+  if (!dev && n > 0) {
+    IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
+    if (fk_err)
+      IK_HIP(hipMemcpyAsync(fk_err, de, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  return finish(c, flags, stats);
+}
+
+}  // extern "C"

@@ -1,0 +1,254 @@
+// ik_common.h -- device helpers shared by the FK / FABRIK / ANN kernels.
+//
+// Float64 arithmetic here follows the reference's operation order exactly and
+// the whole library is compiled with -ffp-contract=off (CPython never fuses a
+// multiply-add), so that FABRIK iteration counts match the reference bit for
+// bit.  The one deliberate difference: the reference squares with pow(v, 2)
+// (glibc pow, kinematics/point.py:27-29, inverse.py:79,90,98), here v*v, the
+// correctly rounded square; glibc pow differs from it in the last ulp on a
+// small fraction of inputs.  See DESIGN.md "Numerics".
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ikhip.h"
+
+namespace ikhip {
+
+constexpr double kPi = 3.141592653589793;  // math.pi
+
+// Device-side accumulators of one call (reset by reset_stats_kernel).
+struct DevStats {
+  unsigned long long first_oob;      // atomicMin of point index
+  unsigned long long first_err_key;  // atomicMin of (index << 8) | code
+  unsigned long long sum_iters;
+  unsigned long long n_capped;
+  unsigned long long max_fk_err_bits;  // atomicMax on the bits of a non-negative double
+  double sum_fk_err;
+  int max_iters;
+  int pad0;
+  unsigned long long queue;  // work-queue head (persistent kernels)
+};
+
+struct d3 {
+  double x, y, z;
+};
+
+// The reference's pow(v, 2).
+__device__ __forceinline__ double sq(double v) { return v * v; }
+
+// kinematics/point.py:25-29 get_distance_between
+__device__ __forceinline__ double dist3(d3 a, d3 b) {
+  return sqrt(sq(a.x - b.x) + sq(a.y - b.y) + sq(a.z - b.z));
+}
+
+__device__ __forceinline__ void set_err(int &st, int code) {
+  if (st == IK_OK) st = code;
+}
+
+// kinematics/point.py:32-45 get_point_between: s_c + ((d / |s-e|) * (e_c - s_c)).
+// |s-e| == 0 raises ZeroDivisionError in the reference.
+__device__ __forceinline__ d3 point_between(d3 s, d3 e, double d, int &st) {
+  double n = dist3(s, e);
+  if (n == 0.0) set_err(st, IK_E_ZERODIV);
+  double q = d / n;
+  d3 r;
+  r.x = s.x + (q * (e.x - s.x));
+  r.y = s.y + (q * (e.y - s.y));
+  r.z = s.z + (q * (e.z - s.z));
+  return r;
+}
+
+// CPython round(v, 8): exact value of v rounded half-even to 8 decimals, then
+// the nearest double.  v*1e8 = p + e exactly; e breaks a tie at p = k + 1/2.
+__device__ __forceinline__ double py_round8(double v) {
+  const double s = 1e8;
+  double p = v * s;
+  if (!isfinite(p)) return v;
+  double e = fma(v, s, -p);
+  double fl = floor(p);
+  double k;
+  if (p - fl == 0.5) {
+    k = (e > 0) ? fl + 1.0 : ((e < 0) ? fl : rint(p));
+  } else {
+    k = rint(p);
+  }
+  double r = k / s;
+  if (r == 0.0) r = copysign(0.0, v);
+  return r;
+}
+
+// math.acos: ValueError('math domain error') outside [-1, 1]; nan passes.
+__device__ __forceinline__ double py_acos(double v, int &st) {
+  if (v > 1.0 || v < -1.0) set_err(st, IK_E_DOMAIN);
+  return acos(v);
+}
+
+// float division: ZeroDivisionError when the divisor is zero.
+__device__ __forceinline__ double py_div(double a, double b, int &st) {
+  if (b == 0.0) set_err(st, IK_E_ZERODIV);
+  return a / b;
+}
+
+// ---------------------------------------------------------------- FK ----
+// kinematics/forward.py:21-94.  A_i = Rz(theta)*Tz(d)*Tx(a)*Rx(alpha) and the
+// chain M_{i+1} = M_i * A_{i+1}, each 4x4 product an FMA chain in k order from
+// 0 (what numpy's dgemm does; pinned bit-exact by the oracle tests).
+__device__ __forceinline__ void mm4(const double *A, const double *B, double *C) {
+  double T[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = fma(A[i * 4 + k], B[k * 4 + j], acc);
+      T[i * 4 + j] = acc;
+    }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) C[i] = T[i];
+}
+
+__device__ __forceinline__ void ident4(double *M) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) M[i] = (i % 5 == 0) ? 1.0 : 0.0;
+}
+
+__device__ __forceinline__ bool angle_ok(double a) { return !((a < -2 * kPi) || (a > 2 * kPi)); }
+
+__device__ __forceinline__ void dh_transform(double th, double eps, double a, double al,
+                                             double *A) {
+  double R[16], T1[16], T2[16], X[16];
+  double c = cos(th), s = sin(th);
+  ident4(R);
+  R[0] = c; R[1] = -s; R[4] = s; R[5] = c;
+  ident4(T1);
+  T1[11] = eps;
+  ident4(T2);
+  T2[3] = a;
+  double ca = cos(al), sa = sin(al);
+  ident4(X);
+  X[5] = ca; X[6] = -sa; X[9] = sa; X[10] = ca;
+  mm4(R, T1, A);
+  mm4(A, T2, A);
+  mm4(A, X, A);
+}
+
+// dh: rows thetas(unused here), d, a, alpha; th: the 4 joint angles.
+// Writes the translations of M_1..M_4.  Returns IK_OK or IK_E_ANGLE_RANGE.
+__device__ __forceinline__ int fk_chain(const double *dh, const double th[4], d3 J[4]) {
+  int st = IK_OK;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (!angle_ok(th[i]) || !angle_ok(dh[12 + i])) st = IK_E_ANGLE_RANGE;
+  double M[16], A[16];
+  dh_transform(th[0], dh[4], dh[8], dh[12], M);
+  J[0].x = M[3]; J[0].y = M[7]; J[0].z = M[11];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    dh_transform(th[i], dh[4 + i], dh[8 + i], dh[12 + i], A);
+    mm4(M, A, M);
+    J[i].x = M[3]; J[i].y = M[7]; J[i].z = M[11];
+  }
+  return st;
+}
+
+// Same chain, writing all four cumulative transforms (row-major 4x4 each).
+__device__ __forceinline__ int fk_chain_mats(const double *dh, const double th[4], double *out) {
+  int st = IK_OK;
+  for (int i = 0; i < 4; ++i)
+    if (!angle_ok(th[i]) || !angle_ok(dh[12 + i])) st = IK_E_ANGLE_RANGE;
+  double M[16], A[16];
+  dh_transform(th[0], dh[4], dh[8], dh[12], M);
+  for (int k = 0; k < 16; ++k) out[k] = M[k];
+  for (int i = 1; i < 4; ++i) {
+    dh_transform(th[i], dh[4 + i], dh[8 + i], dh[12 + i], A);
+    mm4(M, A, M);
+    for (int k = 0; k < 16; ++k) out[16 * i + k] = M[k];
+  }
+  return st;
+}
+
+// ------------------------------------------------------------- stats ----
+__device__ __forceinline__ void record_error(DevStats *S, int64_t idx, int code) {
+  unsigned long long key = ((unsigned long long)idx << 8) | (unsigned long long)code;
+  atomicMin(&S->first_err_key, key);
+}
+
+__device__ __forceinline__ bool outside(const double *lim, double x, double y, double z) {
+  // kinematics/inverse.py:26-35: inclusive bounds, dict order x, y, z
+  return (x < lim[0] || x > lim[1]) || (y < lim[2] || y > lim[3]) || (z < lim[4] || z > lim[5]);
+}
+
+// 64-lane wave sum of a 64-bit value.
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+}  // namespace ikhip
+
+// Launchers implemented in the .hip files and called by ik_api.cpp.
+namespace ikhip {
+struct RobotDev {
+  double dh[16];
+  double links[4];
+  double lim[6];
+};
+
+// Optional per-kernel HIP-event timing of the current call (ik_ctx_set_timing):
+// launchers bracket every kernel with kt_begin / kt_end.
+void kt_begin(const char *name, hipStream_t st);
+void kt_end(hipStream_t st);
+
+void launch_reset_stats(DevStats *S, hipStream_t st);
+void launch_check_limits(const RobotDev &r, const double *pts, int64_t n, DevStats *S,
+                         hipStream_t st);
+void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, double *mats,
+               DevStats *S, hipStream_t st);
+// FABRIK ikine.  scratch must hold fabrik_scratch_bytes(n).
+size_t fabrik_scratch_bytes(int64_t n);
+void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
+                         int max_iter, double *ang, int32_t *iters, double *joints,
+                         bool check_limits, void *scratch, DevStats *S, hipStream_t st,
+                         int variant);
+void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,
+                        const double *goals, int64_t n, double tol, int max_iter,
+                        double *joints, int32_t *iters, DevStats *S, hipStream_t st);
+
+constexpr int kAnnMaxLayers = 24;
+constexpr int kAnnMaxWidth = 512;
+struct AnnModelDev {
+  int n_layers;
+  int kp[kAnnMaxLayers];  // padded in-dim (multiple of 8)
+  int np[kAnnMaxLayers];  // padded out-dim (multiple of 32)
+  int act[kAnnMaxLayers];
+  const float4 *wp[kAnnMaxLayers];  // packed weights (see ik_ann.hip)
+  const float *bias[kAnnMaxLayers];
+  double xm[3], xs[3], ym[4], ys[4];
+};
+size_t ann_packed_floats(int k, int n);  // floats of one packed layer
+void ann_pack_layer(const float *W, int k, int n, float *dst);  // host-side packing
+void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
+                float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st);
+}  // namespace ikhip

@@ -1,0 +1,407 @@
+// ik_fabrik.hip -- batched FABRIK inverse kinematics for gfx950.
+//
+// Restates, one goal point per lane in float64, the reference's
+//   FabrikInverseKinematics.ikine   kinematics/inverse.py:115-139
+//   Fabrik.calculate / __backward / __forward   kinematics/fabrik.py:19-67
+//   __get_angles                    kinematics/inverse.py:54-112
+// with the same operation order, so iteration counts are bit-exact.
+//
+// Two pipelines (DESIGN.md "FABRIK"):
+//  * split (default): seed_kernel (limits + FK seed pose) -> iter_kernel
+//    (persistent; a lane whose point converged is refilled from a per-wave
+//    chunk of a global work queue, so a wave no longer waits for its slowest
+//    lane) -> angles_kernel (law of cosines + per-batch stats).
+//  * simple: everything in one kernel, one point per lane, no refill.
+// Per point the state is 4 joints + goal (15 doubles) held in VGPRs.
+#include "ik_common.h"
+
+namespace ikhip {
+
+// One FABRIK iteration for the 4-joint chain (fabrik.py:57-64): backward pass
+// from the goal (dists[2], dists[1], dists[0]), start error, forward pass from
+// the start (dists[1], dists[2], dists[3]), goal error.  cur[0] is always start.
+__device__ __forceinline__ void fabrik_step4(const d3 start, d3 &c1, d3 &c2, d3 &c3,
+                                             const d3 g, const double *L, double &se,
+                                             double &ge, int &st) {
+  d3 b2 = point_between(g, c2, L[2], st);
+  d3 b1 = point_between(b2, c1, L[1], st);
+  d3 b0 = point_between(b1, start, L[0], st);
+  se = dist3(b0, start);
+  c1 = point_between(start, b1, L[1], st);
+  c2 = point_between(c1, b2, L[2], st);
+  c3 = point_between(c2, g, L[3], st);
+  ge = dist3(c3, g);
+}
+
+// kinematics/inverse.py:54-112 __get_angles; J = FABRIK joints B, C, D, E.
+__device__ __forceinline__ void get_angles(const d3 J[4], double th[4], int &st) {
+  const d3 A = {0.0, 0.0, 0.0};
+  const d3 B = J[0], C = J[1], D = J[2], E = J[3];
+  th[0] = atan2(E.y, E.x);
+  double ab = dist3(A, B), bc = dist3(B, C), cd = dist3(C, D), de = dist3(D, E);
+  double ac = dist3(A, C);
+  double num = (sq(ab) + sq(bc)) - sq(ac);
+  double den = 2 * ab * bc;
+  double a2 = py_acos(py_round8(py_div(num, den, st)), st);
+  th[1] = (C.x * D.x < 0) ? ((3 * kPi / 2) - a2) : -(kPi / 2 - a2);
+  double bd = dist3(B, D);
+  num = (sq(bc) + sq(cd)) - sq(bd);
+  den = 2 * bc * cd;
+  double a3 = py_acos(py_round8(py_div(num, den, st)), st);
+  th[2] = -(kPi - a3);
+  double ce = dist3(C, E);
+  num = (sq(cd) + sq(de)) - sq(ce);
+  den = 2 * cd * de;
+  double a4 = py_acos(py_round8(py_div(num, den, st)), st);
+  d3 m = point_between(C, E, dist3(C, E) / 2, st);
+  double da = dist3(B, m);
+  double db = dist3(B, D);
+  th[3] = (db > da) ? -(kPi - a4) : (kPi - a4);
+}
+
+// Seed pose, inverse.py:123-130: FK of [atan2(y, x), thetas[1:]] (the
+// reference writes theta_1 into dh_matrix[0][0] and runs fkine on that row).
+__device__ __forceinline__ int seed_pose(const RobotDev &r, d3 g, d3 J[4]) {
+  double th[4] = {atan2(g.y, g.x), r.dh[1], r.dh[2], r.dh[3]};
+  return fk_chain(r.dh, th, J);
+}
+
+__device__ __forceinline__ void store_joints(double *dst, int64_t i, const d3 J[4]) {
+  double *p = dst + 12 * i;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    p[3 * k] = J[k].x;
+    p[3 * k + 1] = J[k].y;
+    p[3 * k + 2] = J[k].z;
+  }
+}
+
+__device__ __forceinline__ void load_joints(const double *src, int64_t i, d3 J[4]) {
+  const double2 *p = reinterpret_cast<const double2 *>(src + 12 * i);
+  double2 v0 = p[0], v1 = p[1], v2 = p[2], v3 = p[3], v4 = p[4], v5 = p[5];
+  J[0] = {v0.x, v0.y, v1.x};
+  J[1] = {v1.y, v2.x, v2.y};
+  J[2] = {v3.x, v3.y, v4.x};
+  J[3] = {v4.y, v5.x, v5.y};
+}
+
+// Per-wave FABRIK stats -> one atomic each per wave.
+__device__ __forceinline__ void wave_iter_stats(DevStats *S, bool valid, int it, int max_iter) {
+  unsigned long long s = valid ? (unsigned long long)it : 0ull;
+  unsigned long long c = (valid && it >= max_iter) ? 1ull : 0ull;
+  int m = valid ? it : 0;
+  s = wave_sum_u64(s);
+  c = wave_sum_u64(c);
+  m = wave_max_i32(m);
+  if ((threadIdx.x & 63) == 0) {
+    if (s) atomicAdd(&S->sum_iters, s);
+    if (c) atomicAdd(&S->n_capped, c);
+    if (m) atomicMax(&S->max_iters, m);
+  }
+}
+
+struct FabArgs {
+  RobotDev r;
+  const double *pts;
+  int64_t n;
+  double tol;
+  int max_iter;
+  int check_limits;
+  double *ang;
+  int32_t *iters;
+  double *joints;  // final joints (n x 12); never null in the split pipeline
+  double *seeds;   // split pipeline scratch (n x 12)
+  uint8_t *status; // split pipeline scratch (n)
+  DevStats *S;
+};
+
+// ------------------------------------------------------------- simple ----
+__global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool valid = i < a.n;
+  int it = 0;
+  if (valid) {
+    d3 g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
+    if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
+      atomicMin(&a.S->first_oob, (unsigned long long)i);
+    d3 J[4];
+    int st = seed_pose(a.r, g, J);
+    double se = 1.0, ge = 1.0;
+    if (st == IK_OK) {
+      while (((se > a.tol) || (ge > a.tol)) && (a.max_iter > it)) {
+        fabrik_step4(J[0], J[1], J[2], J[3], g, a.r.links, se, ge, st);
+        ++it;
+        if (st != IK_OK) break;
+      }
+    }
+    double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
+    if (st == IK_OK) get_angles(J, th, st);
+    if (st != IK_OK) record_error(a.S, i, st);
+    double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
+    o[0] = make_double2(th[0], th[1]);
+    o[1] = make_double2(th[2], th[3]);
+    if (a.iters) a.iters[i] = it;
+    if (a.joints) store_joints(a.joints, i, J);
+  }
+  wave_iter_stats(a.S, valid, it, a.max_iter);
+}
+
+// -------------------------------------------------------------- split ----
+// 1. limits + seed pose (uniform work, one point per lane)
+__global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  d3 g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
+  if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
+    atomicMin(&a.S->first_oob, (unsigned long long)i);
+  d3 J[4];
+  int st = seed_pose(a.r, g, J);
+  store_joints(a.seeds, i, J);
+  a.status[i] = (uint8_t)st;
+}
+
+// 2. persistent iteration with per-lane refill.
+constexpr int kQueueChunk = 512;  // points a wave takes from the global queue at once
+
+template <int REFILL_MIN>
+__global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const double tol = a.tol;
+  const int max_iter = a.max_iter;
+  double L[4] = {a.r.links[0], a.r.links[1], a.r.links[2], a.r.links[3]};
+
+  int64_t qnext = 0, qend = 0;  // wave-uniform: indices not yet handed out
+  bool exhausted = false;
+  bool active = false;
+  int64_t idx = 0;
+  d3 J0 = {0, 0, 0}, J1 = J0, J2 = J0, J3 = J0, g = J0;
+  double se = 1.0, ge = 1.0;
+  int step = 0, st = IK_OK;
+
+  while (true) {
+    unsigned long long freem = __ballot(!active);
+    int nfree = __popcll(freem);
+    if (exhausted && nfree == 64) break;
+    if (!exhausted && (nfree >= REFILL_MIN || nfree == 64)) {
+      int rank = __popcll(freem & lt_mask);
+      int64_t mine = -1;
+      int handed = 0;
+      while (handed < nfree) {
+        if (qnext >= qend) {
+          unsigned long long old = 0;
+          if (lane == 0) old = atomicAdd(&a.S->queue, (unsigned long long)kQueueChunk);
+          old = __shfl(old, 0, 64);
+          if ((int64_t)old >= a.n) {
+            exhausted = true;
+            break;
+          }
+          qnext = (int64_t)old;
+          qend = min((int64_t)old + kQueueChunk, a.n);
+        }
+        int take = (int)min((int64_t)(nfree - handed), qend - qnext);
+        if (!active && rank >= handed && rank < handed + take) mine = qnext + (rank - handed);
+        qnext += take;
+        handed += take;
+      }
+      if (mine >= 0) {
+        idx = mine;
+        d3 Jn[4];
+        load_joints(a.seeds, idx, Jn);
+        J0 = Jn[0]; J1 = Jn[1]; J2 = Jn[2]; J3 = Jn[3];
+        g = {a.pts[3 * idx], a.pts[3 * idx + 1], a.pts[3 * idx + 2]};
+        st = a.status[idx];
+        se = 1.0;
+        ge = 1.0;
+        step = 0;
+        active = true;
+      }
+    }
+    if (active) {
+      if (st == IK_OK && ((se > tol) || (ge > tol)) && (max_iter > step)) {
+        fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
+        ++step;
+      } else {
+        d3 J[4] = {J0, J1, J2, J3};
+        store_joints(a.joints, idx, J);
+        a.iters[idx] = step;
+        a.status[idx] = (uint8_t)st;
+        active = false;
+      }
+    }
+  }
+}
+
+// 3. angles + stats (uniform work, one point per lane)
+__global__ __launch_bounds__(256) void fabrik_angles_kernel(FabArgs a) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool valid = i < a.n;
+  int it = 0;
+  if (valid) {
+    int st = a.status[i];
+    it = a.iters[i];
+    double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
+    if (st == IK_OK) {
+      d3 J[4];
+      load_joints(a.joints, i, J);
+      get_angles(J, th, st);
+    }
+    if (st != IK_OK) record_error(a.S, i, st);
+    double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
+    o[0] = make_double2(th[0], th[1]);
+    o[1] = make_double2(th[2], th[3]);
+  }
+  wave_iter_stats(a.S, valid, it, a.max_iter);
+}
+
+size_t fabrik_scratch_bytes(int64_t n) {
+  // seeds n*12 doubles, joints n*12 doubles, iters n int32, status n bytes
+  size_t b = 0;
+  b += (size_t)n * 96;
+  b += (size_t)n * 96;
+  b += ((size_t)n * 4 + 255) & ~(size_t)255;
+  b += ((size_t)n + 255) & ~(size_t)255;
+  return b + 1024;
+}
+
+static int g_cus = 0;
+static int num_cus() {
+  if (g_cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        g_cus <= 0)
+      g_cus = 256;
+  }
+  return g_cus;
+}
+
+void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
+                         int max_iter, double *ang, int32_t *iters, double *joints,
+                         bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
+                         int variant) {
+  if (n <= 0) return;
+  FabArgs a;
+  a.r = r;
+  a.pts = pts;
+  a.n = n;
+  a.tol = tol;
+  a.max_iter = max_iter;
+  a.check_limits = check_limits ? 1 : 0;
+  a.ang = ang;
+  a.iters = iters;
+  a.joints = joints;
+  a.S = S;
+  unsigned grid = (unsigned)((n + 255) / 256);
+  if (variant == 0) {
+    a.seeds = nullptr;
+    a.status = nullptr;
+    kt_begin("fabrik_simple_kernel", stream);
+    hipLaunchKernelGGL(fabrik_simple_kernel, dim3(grid), dim3(256), 0, stream, a);
+    kt_end(stream);
+    return;
+  }
+  char *p = static_cast<char *>(scratch);
+  a.seeds = reinterpret_cast<double *>(p);
+  p += (size_t)n * 96;
+  double *jtmp = reinterpret_cast<double *>(p);
+  p += (size_t)n * 96;
+  int32_t *itmp = reinterpret_cast<int32_t *>(p);
+  p += ((size_t)n * 4 + 255) & ~(size_t)255;
+  a.status = reinterpret_cast<uint8_t *>(p);
+  if (!a.joints) a.joints = jtmp;
+  if (!a.iters) a.iters = itmp;
+  kt_begin("fabrik_seed_kernel", stream);
+  hipLaunchKernelGGL(fabrik_seed_kernel, dim3(grid), dim3(256), 0, stream, a);
+  kt_end(stream);
+  unsigned pgrid = (unsigned)num_cus() * 8;
+  int64_t waves_needed = (n + 63) / 64;
+  if ((int64_t)pgrid * 4 > waves_needed)
+    pgrid = (unsigned)((waves_needed + 3) / 4 > 0 ? (waves_needed + 3) / 4 : 1);
+  kt_begin("fabrik_iter_kernel", stream);
+  if (variant == 2)
+    hipLaunchKernelGGL(fabrik_iter_kernel<1>, dim3(pgrid), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(fabrik_iter_kernel<8>, dim3(pgrid), dim3(256), 0, stream, a);
+  kt_end(stream);
+  kt_begin("fabrik_angles_kernel", stream);
+  hipLaunchKernelGGL(fabrik_angles_kernel, dim3(grid), dim3(256), 0, stream, a);
+  kt_end(stream);
+}
+
+// ------------------------------------------------------ Fabrik.calculate ----
+template <int NJ>
+__global__ __launch_bounds__(256) void fabrik_calc_kernel(const double *dists_in,
+                                                          const double *init, int shared,
+                                                          const double *goals, int64_t n,
+                                                          double tol, int max_iter,
+                                                          double *joints, int32_t *iters,
+                                                          DevStats *S) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool valid = i < n;
+  int it = 0;
+  if (valid) {
+    double L[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) L[k] = dists_in[k];
+    const double *ip = shared ? init : init + (size_t)i * NJ * 3;
+    d3 cur[NJ], B[NJ];
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) cur[k] = {ip[3 * k], ip[3 * k + 1], ip[3 * k + 2]};
+    d3 g = {goals[3 * i], goals[3 * i + 1], goals[3 * i + 2]};
+    const d3 start = cur[0];
+    double se = 1.0, ge = 1.0;
+    int st = IK_OK;
+    while (((se > tol) || (ge > tol)) && (max_iter > it)) {
+      B[NJ - 1] = g;
+#pragma unroll
+      for (int k = NJ - 2; k >= 0; --k) B[k] = point_between(B[k + 1], cur[k], L[k], st);
+      se = dist3(B[0], start);
+      cur[0] = start;
+#pragma unroll
+      for (int k = 1; k < NJ; ++k) cur[k] = point_between(cur[k - 1], B[k], L[k], st);
+      ge = dist3(cur[NJ - 1], g);
+      ++it;
+      if (st != IK_OK) break;
+    }
+    if (st != IK_OK) record_error(S, i, st);
+    double *o = joints + (size_t)i * NJ * 3;
+#pragma unroll
+    for (int k = 0; k < NJ; ++k) {
+      o[3 * k] = cur[k].x;
+      o[3 * k + 1] = cur[k].y;
+      o[3 * k + 2] = cur[k].z;
+    }
+    if (iters) iters[i] = it;
+  }
+  wave_iter_stats(S, valid, it, max_iter);
+}
+
+void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,
+                        const double *goals, int64_t n, double tol, int max_iter,
+                        double *joints, int32_t *iters, DevStats *S, hipStream_t st) {
+  if (n <= 0) return;
+  unsigned grid = (unsigned)((n + 255) / 256);
+  int sh = init_shared ? 1 : 0;
+#define IK_CALC_CASE(K)                                                                      \
+  case K:                                                                                    \
+    hipLaunchKernelGGL(fabrik_calc_kernel<K>, dim3(grid), dim3(256), 0, st, dists, init, sh, \
+                       goals, n, tol, max_iter, joints, iters, S);                           \
+    break;
+  kt_begin("fabrik_calc_kernel", st);
+  switch (nj) {
+    IK_CALC_CASE(2)
+    IK_CALC_CASE(3)
+    IK_CALC_CASE(4)
+    IK_CALC_CASE(5)
+    IK_CALC_CASE(6)
+    IK_CALC_CASE(7)
+    IK_CALC_CASE(8)
+    default:
+      break;
+  }
+  kt_end(st);
+#undef IK_CALC_CASE
+}
+
+}  // namespace ikhip

@@ -1,0 +1,270 @@
+"""GPU parity: libikhip (HIP, gfx950) against the CPU oracle and the reference's
+golden fixtures.  Tolerances (north_star: 1e-5 absolute on angles, bit-exact
+FABRIK iteration counts) are written next to each assert; where the kernels do
+better than the contract the tighter bound is asserted too.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+NS_TOL = 1e-5  # north_star angle tolerance (float), absolute
+
+
+def _load(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+@pytest.fixture(scope="module", params=[1, 0, 2], ids=["split", "simple", "split_refill1"])
+def ctx(request):
+    from inversekinematicsann_amd import _native
+    os.environ["IKHIP_FABRIK_VARIANT"] = str(request.param)
+    c = _native.Context(0)
+    os.environ.pop("IKHIP_FABRIK_VARIANT", None)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def ctx1():
+    from inversekinematicsann_amd import _native
+    c = _native.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("name", ["fabrik_random_dist_tol1e-3.npz",
+                                  "fabrik_random_dist_tol1e-5_it200.npz",
+                                  "fabrik_uniform_box.npz", "fabrik_spring20.npz"])
+def test_fabrik_vs_reference_golden(ctx, name):
+    g = _load(name)
+    ang, it, jo, st = ctx.fabrik_solve(g["points"], float(g["tol"]), int(g["max_iter"]),
+                                       want_joints=True)
+    assert st.first_oob == -1 and st.first_err == -1
+    assert np.array_equal(it, g["iters"])                       # bit-exact counts
+    assert np.abs(ang - g["angles"]).max() <= NS_TOL            # contract
+    assert np.abs(ang - g["angles"]).max() <= 1e-9              # achieved
+    assert np.abs(jo - g["joints"]).max() <= 1e-9
+    assert st.sum_iters == int(g["iters"].sum())
+    assert st.max_iters == int(g["iters"].max())
+    assert st.n_capped == int((g["iters"] >= int(g["max_iter"])).sum())
+
+
+def test_fabrik_vs_oracle_random(ctx):
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    pts = random_dist(50_000, seed=3)
+    for tol, mi in ((1e-3, 100), (1e-5, 200)):
+        ang, it, jo, st = ctx.fabrik_solve(pts, tol, mi, want_joints=True)
+        rang, rit, rjo, rst = O.fabrik_ikine(pts, tol, mi)
+        assert np.array_equal(it, rit)
+        assert np.abs(ang - rang).max() <= 1e-9
+        assert np.abs(jo - rjo).max() <= 1e-9
+
+
+def test_fabrik_ragged_sizes(ctx):
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    for n in (1, 63, 64, 65, 255, 257, 1000, 4097):
+        pts = random_dist(n, seed=n)
+        ang, it, _, st = ctx.fabrik_solve(pts, 1e-3, 100)
+        rang, rit, _, _ = O.fabrik_ikine(pts, 1e-3, 100)
+        assert np.array_equal(it, rit), n
+        assert np.abs(ang - rang).max() <= 1e-9, n
+    ang, it, _, st = ctx.fabrik_solve(np.zeros((0, 3)), 1e-3, 100)
+    assert ang.shape == (0, 4)
+
+
+def test_fabrik_edge_cases_and_errors(ctx):
+    with open(os.path.join(GOLDEN, "fabrik_edge.json")) as f:
+        d = json.load(f)
+    for rec in d["edge"]:
+        p = np.array([rec["point"]])
+        ang, it, _, st = ctx.fabrik_solve(p, 1e-3, 100)
+        exc = rec["exception"]
+        if exc == "OutOfRobotReachException":
+            assert st.first_oob == 0
+        elif exc == "ZeroDivisionError":
+            assert st.first_err == 0 and st.first_err_code == 3
+        elif exc == "ValueError":
+            assert st.first_err == 0 and st.first_err_code == 2
+        else:
+            assert st.first_err == -1 and st.first_oob == -1
+            assert it[0] == rec["iters"]
+            assert np.abs(ang[0] - np.array(rec["angles"])).max() <= 1e-9
+
+
+def test_fabrik_error_precedence(ctx):
+    # a ZeroDivision point (index 1) before an out-of-reach point (index 2):
+    # the reference checks limits for the whole batch first.
+    pts = np.array([[1.0, 2.0, 3.0], [0.0, 0.0, 2.0], [1.0, 2.1, -3.123], [1.0, 2.0, 7.0]])
+    _, _, _, st = ctx.fabrik_solve(pts, 1e-3, 100)
+    assert st.first_oob == 2
+    _, _, _, st = ctx.fabrik_solve(pts[:2], 1e-3, 100)
+    assert st.first_oob == -1 and st.first_err == 1 and st.first_err_code == 3
+
+
+def test_fabrik_api_dropin():
+    """kinematics.inverse-style usage, mirroring tests/inverse_unit.py:15-34."""
+    from inversekinematicsann_amd.kinematics.inverse import FabrikInverseKinematics
+    from inversekinematicsann_amd.robot.robot import SixDOFRobot, OutOfRobotReachException
+    robot = SixDOFRobot()
+    dh = [list(r) for r in robot.dh_matrix]
+    ik = FabrikInverseKinematics(dh, robot.links_lengths, robot.effector_workspace_limits)
+    points = [[1.0, 2.1, 3.0], [1.567, 2.22, -2.123], [1.02, 3.33, 4.99]]
+    output = [[1.1263771168937977, 1.95663870779144, -1.581170282866297, -1.2914981807424972],
+              [0.9561510602151175, -0.1334947854494175, -1.441291844752837,
+               0.38467252287989595],
+              [1.2735640189772053, 1.4953811089376177, -0.6880936114216039, -1.03376967052818]]
+    predicted = ik.ikine(points)
+    assert isinstance(predicted, list) and isinstance(predicted[0][0], float)
+    np.testing.assert_almost_equal(predicted, output, decimal=6)
+    with open(os.path.join(GOLDEN, "fabrik_edge.json")) as f:
+        d = json.load(f)
+    assert dh[0][0] == math.atan2(3.33, 1.02)  # last point's theta_1
+    with pytest.raises(OutOfRobotReachException) as ei:
+        ik.ikine(d["batch"])
+    assert str(ei.value) == d["batch_exception"]["message"]
+    with pytest.raises(ZeroDivisionError):
+        ik.ikine([[1.0, 2.0, 3.0], [0.0, 0.0, 2.0]])
+
+
+def test_fabrik_calc_generic_chain(ctx1):
+    g = _load("fabrik_calc_5joint.npz")
+    out, it, st = ctx1.fabrik_calc(g["links"], g["init"], g["goals"], float(g["tol"]),
+                                   int(g["max_iter"]))
+    assert np.array_equal(it, g["iters"])
+    assert np.abs(out - g["joints"]).max() <= 1e-9
+
+
+def test_fabrik_calculate_dropin():
+    """tests/fabrik_unit.py:17-41 through the GPU Fabrik class."""
+    from inversekinematicsann_amd.kinematics.fabrik import Fabrik
+    from inversekinematicsann_amd.kinematics.forward import ForwardKinematics
+    from inversekinematicsann_amd.kinematics.point import Point
+    from inversekinematicsann_amd.robot.robot import SixDOFRobot
+    robot = SixDOFRobot()
+    fab = Fabrik(robot.links_lengths)
+    fk = ForwardKinematics([list(r) for r in robot.dh_matrix])
+    _, fkall = fk.fkine([0, math.pi / 2, 0, 0])
+    start = [Point([m[0, 3], m[1, 3], m[2, 3]]) for m in fkall]
+    calc = fab.calculate(start, [1, 2, 3])
+    np.testing.assert_array_almost_equal(
+        calc[3], [1.0000000035582093, 2.0000000071394073, 2.999999989135574])
+    with pytest.raises(ValueError):
+        fab.calculate(start[:3], [1, 2, 3])
+
+
+def test_fk_vs_reference_golden(ctx1):
+    g = _load("fk_random.npz")
+    xyz, mats, st = ctx1.fk(g["angles"], with_mats=True)
+    assert st.first_err == -1
+    assert np.abs(xyz - g["joints"][:, 3]).max() <= 1e-12
+    assert np.abs(mats[:, :, :3, 3] - g["joints"]).max() <= 1e-12
+    # forward_unit.py:18-31
+    dest = [[1.34542, 2.99821, 3.67401], [0.01333, -3.72111, -1.09902],
+            [3.95444, -1.00112, 1.00378]]
+    angs = [[1.1489898108341745, 1.6426609377538854, -1.2027772444264693, -1.0663073873609727],
+            [-1.5672140776862065, 0.2433182869870163, -1.3760689820099818, 0.0465569704233757],
+            [-0.24795388218721454, 0.9644220067435634, -1.5389903144536021,
+             -0.3143083371860276]]
+    xyz, _, _ = ctx1.fk(np.array(angs))
+    np.testing.assert_array_almost_equal(xyz, dest, decimal=4)
+    _, _, st = ctx1.fk(np.array([[0.0, 0.0, 0.0, 0.0], [7.0, 0, 0, 0]]))
+    assert st.first_err == 1 and st.first_err_code == 4
+
+
+# ------------------------------------------------------------------ ANN ----
+def _ann_case(ctx, dims, acts_hidden, n, seed, check_limits=False, fk=False):
+    from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER as XS, \
+        REFERENCE_Y_SCALER as YS
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    m = glorot_model(dims=dims, seed=seed, hidden_act=acts_hidden)
+    rng = np.random.default_rng(seed)
+    for b in m.biases:
+        b[:] = rng.normal(0, 0.1, b.shape).astype(np.float32)
+    ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    pts = random_dist(n, seed=seed)
+    ang, err, st = ctx.ann_solve(pts, check_limits=check_limits, want_fk_err=fk)
+    ref64 = O.ann_forward(pts, m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean,
+                          YS.scale, compute=np.float64)
+    return m, pts, ang, err, st, ref64
+
+
+@pytest.mark.parametrize("dims,act", [
+    ((3,) + (500,) * 12 + (4,), "tanh"),       # the reference architecture, ann.py:46-56
+    ((3, 64, 4), "tanh"),
+    ((3, 100, 37, 250, 4), "tanh"),             # ragged widths: every NR path
+    ((3, 512, 512, 4), "relu"),
+    ((3, 96, 96, 4), "sigmoid"),
+    ((3, 4), "linear"),
+])
+def test_ann_vs_oracle(ctx1, dims, act):
+    n = 4099  # not a multiple of the 64-point tile
+    m, pts, ang, _, st, ref64 = _ann_case(ctx1, dims, act, n, seed=len(dims))
+    assert ang.dtype == np.float32 and ang.shape == (n, 4)
+    d = np.abs(ang.astype(np.float64) - ref64).max()
+    assert d <= NS_TOL, d  # north_star: 1e-5 absolute
+
+
+def test_ann_fk_roundtrip_and_limits(ctx1):
+    dims = (3, 128, 128, 4)
+    m, pts, ang, err, st, ref64 = _ann_case(ctx1, dims, "tanh", 2000, seed=9, fk=True)
+    xyz = O.fk_closed_form(ang.astype(np.float64))
+    ref_err = np.linalg.norm(xyz - pts, axis=1)
+    assert np.abs(err - ref_err).max() <= 1e-9
+    assert st.max_fk_err == pytest.approx(ref_err.max(), rel=1e-12)
+    assert st.sum_fk_err == pytest.approx(ref_err.sum(), rel=1e-9)
+    bad = pts.copy()
+    bad[777, 2] = -3.5
+    bad[1500, 0] = 6.01
+    _, _, st = ctx1.ann_solve(bad, check_limits=True)
+    assert st.first_oob == 777
+
+
+def test_ann_dropin_api():
+    from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER, \
+        REFERENCE_Y_SCALER
+    from inversekinematicsann_amd.kinematics.inverse import AnnInverseKinematics
+    from inversekinematicsann_amd.robot.robot import SixDOFRobot, OutOfRobotReachException
+    robot = SixDOFRobot()
+    ik = AnnInverseKinematics(robot.dh_matrix, robot.links_lengths,
+                              robot.effector_workspace_limits)
+    m = glorot_model(dims=(3, 50, 50, 4), seed=2)
+    ik.ann.set_model(m, REFERENCE_X_SCALER, REFERENCE_Y_SCALER)
+    pts = [[1.0, 2.1, 3.0], [1.567, 2.22, -2.123], [1.02, 3.33, 4.99]]
+    out = ik.ikine(pts)
+    ref = O.ann_forward(pts, m.weights, m.biases, m.activations, REFERENCE_X_SCALER.mean,
+                        REFERENCE_X_SCALER.scale, REFERENCE_Y_SCALER.mean,
+                        REFERENCE_Y_SCALER.scale)
+    assert np.abs(np.array(out) - ref).max() <= NS_TOL
+    assert all(float(np.float32(v)) == v for row in out for v in row)  # fp32 values
+    with pytest.raises(OutOfRobotReachException):
+        ik.ikine([[1.0, 2.1, 3.0], [1.567, 2.22, -3.123], [1.02, 3.33, 4.99]])
+    # ANN.predict has no limit check (ann_unit.py:40 uses an out-of-box point)
+    p = ik.ann.predict([[-1.567, 2.22, -3.123]])
+    assert p.shape == (1, 4) and p.dtype == np.float32
+
+
+def test_device_pointer_path(ctx1):
+    import torch
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    pts = random_dist(10_000, seed=21)
+    dpts = torch.from_numpy(pts).cuda()
+    dang = torch.empty((10_000, 4), dtype=torch.float64, device="cuda")
+    dit = torch.empty(10_000, dtype=torch.int32, device="cuda")
+    ctx1.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx1.fabrik_solve_device(dpts, dang, dit, None, 1e-3, 100,
+                             flags=_native.IK_F_DEVICE | _native.IK_F_ASYNC)
+    st = ctx1.stats_fetch()
+    ctx1.set_stream(None)
+    rang, rit, _, _ = O.fabrik_ikine(pts)
+    assert np.array_equal(dit.cpu().numpy(), rit)
+    assert np.abs(dang.cpu().numpy() - rang).max() <= 1e-9
+    assert st.sum_iters == int(rit.sum())
