@@ -7,16 +7,19 @@
 // plus, in the epilogue, the cli.py:54-61 FK round trip |FK(y) - p|_2 and the
 // inverse.py:26-35 workspace check.
 //
-// Layout (DESIGN.md "ANN"): a workgroup of 4 waves owns a tile of 64 points
-// and carries it through every layer with the activations resident in LDS
-// (64 x 516 fp32, 129 KiB; the 516 stride makes the ds_read_b128 A-fragment
-// reads bank-conflict free).  Each wave computes a 64 x (32*NR) slab of the
-// layer output with v_mfma_f32_32x32x2_f32 (exact fp32, 2x4 accumulator tiles
-// in AGPR/VGPR), streaming its weight columns straight from L2 into registers
-// in a pre-packed "MFMA fragment" order (one 1 KiB dwordx4 load per 8-deep K
-// group and column tile), prefetched one K group ahead.  Bias + activation
-// are applied on the accumulators and written back over the tile in LDS.
-// The grid is persistent: one workgroup per CU walks the point tiles.
+// Layout (DESIGN.md "ANN"): a workgroup of 4 waves owns a tile of BM = 32*MR
+// points and carries it through every layer with the activations resident in
+// LDS (BM x 516 fp32; the 516 stride makes the ds_read_b128 A-fragment reads
+// bank-conflict free).  Each wave computes a BM x (32*NR) slab of the layer
+// output with v_mfma_f32_32x32x2_f32 (exact fp32; MR x NR accumulator tiles),
+// streaming its weight columns straight from L2 into registers in a
+// pre-packed "MFMA fragment" order (one 1 KiB dwordx4 load per 8-deep K group
+// and column tile), triple-buffered two K groups ahead.  Bias + activation are
+// applied on the accumulators and written back over the tile in LDS.
+//   MR = 2: 64-point tiles, 129 KiB LDS, one workgroup per CU (max weight reuse);
+//   MR = 1: 32-point tiles, 64.5 KiB LDS, two workgroups per CU, so one
+//           workgroup's barrier / epilogue overlaps the other's MFMAs.
+// The grid is persistent: workgroups walk the point tiles.
 #include "ik_common.h"
 
 namespace ikhip {
@@ -24,7 +27,6 @@ namespace ikhip {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 64;    // points per tile
 constexpr int kLd = 516;   // LDS row stride in floats (>= 512 + 4)
 constexpr int kWaves = 4;  // waves per workgroup
 
@@ -39,102 +41,106 @@ struct AnnArgs {
   DevStats *S;
 };
 
-// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|); abs error ~1e-7.
+// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|), with the hardware
+// exp2 / reciprocal (1 ulp each): absolute error ~1e-7.
 template <int ACT>
 __device__ __forceinline__ float act_apply(float v) {
   if constexpr (ACT == IK_ACT_TANH) {
-    float e = __expf(-2.0f * fabsf(v));
-    float t = __fdividef(1.0f - e, 1.0f + e);
+    float e = __builtin_amdgcn_exp2f(-2.885390081777927f * fabsf(v));  // exp(-2|v|)
+    float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
     return copysignf(t, v);
   } else if constexpr (ACT == IK_ACT_RELU) {
     return fmaxf(v, 0.0f);
   } else if constexpr (ACT == IK_ACT_SIGMOID) {
-    return __fdividef(1.0f, 1.0f + __expf(-v));
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
   } else {
     return v;
   }
 }
 
-// Operands of one 8-deep K group: A fragments of the two 32-row tiles (LDS)
+// Operands of one 8-deep K group: A fragments of the MR 32-row tiles (LDS)
 // and the B fragments of the wave's NR column tiles (global, packed).
-template <int NR>
+template <int MR, int NR>
 struct Frag {
-  f32x4 a0, a1;
+  f32x4 a[MR];
   f32x4 b[NR];
 };
 
-template <int NR>
-__device__ __forceinline__ void load_group(Frag<NR> &f, const float *a0p, const float *a1p,
+template <int MR, int NR>
+__device__ __forceinline__ void load_group(Frag<MR, NR> &f, const float *ap,
                                            const f32x4 *const (&bp)[NR], int g) {
-  f.a0 = *reinterpret_cast<const f32x4 *>(a0p + 8 * g);
-  f.a1 = *reinterpret_cast<const f32x4 *>(a1p + 8 * g);
+#pragma unroll
+  for (int m = 0; m < MR; ++m) f.a[m] = *reinterpret_cast<const f32x4 *>(ap + m * 32 * kLd + 8 * g);
 #pragma unroll
   for (int j = 0; j < NR; ++j) f.b[j] = bp[j][(size_t)g * 64];
 }
 
-template <int NR>
-__device__ __forceinline__ void mma_group(const Frag<NR> &f, f32x16 (&acc)[2][NR]) {
+template <int MR, int NR>
+__device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[MR][NR]) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
-      acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a0[s], f.b[j][s], acc[0][j], 0, 0, 0);
-      acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a1[s], f.b[j][s], acc[1][j], 0, 0, 0);
+#pragma unroll
+      for (int m = 0; m < MR; ++m)
+        acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[m][s], f.b[j][s], acc[m][j], 0, 0, 0);
     }
   }
 }
 
-// One layer, one wave: out[64 x 32*NR] for the wave's column tiles
-// nt_j = wave + kWaves * j.  G = padded K / 8.  Operands are triple-buffered:
-// the loads of group g+2 are issued before the MFMAs of group g (a scheduling
-// barrier keeps the compiler from sinking them), so ~2 groups (4k cycles of
-// MFMA) cover the L2 / MALL latency of the weight stream.
-template <int NR>
+// One layer, one wave: out[BM x 32*NR] for column tiles nt0 + nt_stride*j over
+// K groups [g0, g1).  The loads of group g+2 are issued before the MFMAs of
+// group g (scheduling barriers keep the compiler from sinking them), so two
+// groups of MFMA cover the L2 / MALL latency of the weight stream.
+template <int MR, int NR>
 __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restrict__ wp, int G,
-                                           int wave, int lane, f32x16 (&acc)[2][NR]) {
+                                           int g0, int g1, int nt0, int nt_stride, int lane,
+                                           f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
-  const float *a0p = H + r * kLd + 4 * h;
-  const float *a1p = H + (32 + r) * kLd + 4 * h;
+  const float *ap = H + r * kLd + 4 * h;
   const f32x4 *bp[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
-    bp[j] = wp + (size_t)(wave + kWaves * j) * G * 64 + lane;
+    bp[j] = wp + (size_t)(nt0 + nt_stride * j) * G * 64 + lane;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) acc[m][j] = (f32x16)(0.0f);
+    for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
   }
-  const int last = G - 1;
-  Frag<NR> f0, f1, f2;
-  load_group(f0, a0p, a1p, bp, 0);
-  load_group(f1, a0p, a1p, bp, min(1, last));
-  int g = 0;
-  for (; g + 3 <= G; g += 3) {
-    load_group(f2, a0p, a1p, bp, min(g + 2, last));
+  if (g1 <= g0) return;
+  const int last = g1 - 1;
+  Frag<MR, NR> f0, f1, f2;
+  load_group(f0, ap, bp, g0);
+  load_group(f1, ap, bp, min(g0 + 1, last));
+  int g = g0;
+  for (; g + 3 <= g1; g += 3) {
+    load_group(f2, ap, bp, min(g + 2, last));
     __builtin_amdgcn_sched_barrier(0);
     mma_group(f0, acc);
     __builtin_amdgcn_sched_barrier(0);
-    load_group(f0, a0p, a1p, bp, min(g + 3, last));
+    load_group(f0, ap, bp, min(g + 3, last));
     __builtin_amdgcn_sched_barrier(0);
     mma_group(f1, acc);
     __builtin_amdgcn_sched_barrier(0);
-    load_group(f1, a0p, a1p, bp, min(g + 4, last));
+    load_group(f1, ap, bp, min(g + 4, last));
     __builtin_amdgcn_sched_barrier(0);
     mma_group(f2, acc);
     __builtin_amdgcn_sched_barrier(0);
   }
-  if (g < G) mma_group(f0, acc);
-  if (g + 1 < G) mma_group(f1, acc);
+  if (g < g1) mma_group(f0, acc);
+  if (g + 1 < g1) mma_group(f1, acc);
 }
 
-template <int NR, int ACT>
+// C/D map of the 32x32 MFMA: column lane & 31, row (q & 3) + 8 (q >> 2) + 4 (lane >> 5).
+template <int MR, int NR, int ACT>
 __device__ __forceinline__ void layer_store(float *H, const float *__restrict__ bias, int wave,
-                                            int lane, const f32x16 (&acc)[2][NR]) {
+                                            int lane, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
+  __syncthreads();  // every wave has finished reading the layer input
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int col = (wave + kWaves * j) * 32 + r;
     const float bv = bias[col];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MR; ++m)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
@@ -143,31 +149,81 @@ __device__ __forceinline__ void layer_store(float *H, const float *__restrict__ 
   }
 }
 
-template <int NR>
+template <int MR, int NR>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wave, int lane) {
-  f32x16 acc[2][NR];
-  layer_gemm<NR>(H, wp, G, wave, lane, acc);
-  __syncthreads();  // every wave has finished reading the layer input
+  f32x16 acc[MR][NR];
+  layer_gemm<MR, NR>(H, wp, G, 0, G, wave, kWaves, lane, acc);
   switch (act) {
-    case IK_ACT_TANH: layer_store<NR, IK_ACT_TANH>(H, bias, wave, lane, acc); break;
-    case IK_ACT_RELU: layer_store<NR, IK_ACT_RELU>(H, bias, wave, lane, acc); break;
-    case IK_ACT_SIGMOID: layer_store<NR, IK_ACT_SIGMOID>(H, bias, wave, lane, acc); break;
-    default: layer_store<NR, IK_ACT_LINEAR>(H, bias, wave, lane, acc); break;
+    case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bias, wave, lane, acc); break;
+    case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bias, wave, lane, acc); break;
+    case IK_ACT_SIGMOID: layer_store<MR, NR, IK_ACT_SIGMOID>(H, bias, wave, lane, acc); break;
+    default: layer_store<MR, NR, IK_ACT_LINEAR>(H, bias, wave, lane, acc); break;
   }
 }
 
-__global__ __launch_bounds__(256, 1) void ann_fused_kernel(AnnArgs a) {
-  __shared__ __attribute__((aligned(16))) float H[kBM * kLd];
+template <int BM, int ACT>
+__device__ __forceinline__ void splitk_finish(float *H, const float *__restrict__ bias, int tid) {
+  for (int o = tid; o < BM * 32; o += kWaves * 64) {
+    const int row = o >> 5, col = o & 31;
+    const float *p = H + row * kLd + 32 + col;
+    float v = ((p[0] + p[32]) + p[64]) + p[96];  // fixed order: deterministic
+    H[row * kLd + col] = act_apply<ACT>(v + bias[col]);
+  }
+}
+
+// A layer with a single 32-column output tile (e.g. the 4-angle output layer,
+// ann.py:56): the K range is split over the 4 waves, the partial BM x 32 tiles
+// go to LDS columns 32..159 (never read by this or the next layer) and are
+// summed in a fixed order, so no wave idles.
+template <int MR>
+__device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, const float *bias,
+                                                 int act, int G, int wave, int lane, int tid) {
+  constexpr int BM = 32 * MR;
+  f32x16 acc[MR][1];
+  const int g0 = (G * wave) / kWaves, g1 = (G * (wave + 1)) / kWaves;
+  layer_gemm<MR, 1>(H, wp, G, g0, g1, 0, 0, lane, acc);
+  __syncthreads();
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+      H[row * kLd + 32 + wave * 32 + r] = acc[m][0][q];
+    }
+  __syncthreads();
+  switch (act) {
+    case IK_ACT_TANH: splitk_finish<BM, IK_ACT_TANH>(H, bias, tid); break;
+    case IK_ACT_RELU: splitk_finish<BM, IK_ACT_RELU>(H, bias, tid); break;
+    case IK_ACT_SIGMOID: splitk_finish<BM, IK_ACT_SIGMOID>(H, bias, tid); break;
+    default: splitk_finish<BM, IK_ACT_LINEAR>(H, bias, tid); break;
+  }
+}
+
+// The FK round trip of one point (cli.py:54-61 + the distance to the target).
+__device__ __forceinline__ double fk_error(const RobotDev &r, const double th[4],
+                                                     double px, double py, double pz) {
+  d3 J[4];
+  int st = fk_chain(r.dh, th, J);
+  d3 p = {px, py, pz};
+  return (st == IK_OK) ? dist3(J[3], p) : __builtin_nan("");
+}
+
+template <int MR>
+__global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnArgs a) {
+  constexpr int BM = 32 * MR;
+  __shared__ __attribute__((aligned(16))) float H[BM * kLd];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
-  const int64_t ntiles = (a.n + kBM - 1) / kBM;
+  const int64_t ntiles = (a.n + BM - 1) / BM;
+  double blk_max = 0.0, blk_sum = 0.0;  // FK round-trip error of this lane's points
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t pt = tile * kBM + tid;
+    const int64_t pt = tile * BM + tid;
     double px = 0.0, py = 0.0, pz = 0.0;
     // ---- input: workspace check + StandardScaler.transform (float64) -> fp32
-    if (tid < kBM) {
+    if (tid < BM) {
       float x0 = 0.0f, x1 = 0.0f, x2 = 0.0f;
       if (pt < a.n) {
         px = a.pts[3 * pt];
@@ -188,21 +244,25 @@ __global__ __launch_bounds__(256, 1) void ann_fused_kernel(AnnArgs a) {
     for (int l = 0; l < a.m.n_layers; ++l) {
       const int G = a.m.kp[l] >> 3;
       const int NT = a.m.np[l] >> 5;
-      const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
       const f32x4 *wp = reinterpret_cast<const f32x4 *>(a.m.wp[l]);
       const float *bias = a.m.bias[l];
       const int act = a.m.act[l];
-      switch (cnt) {
-        case 4: run_layer<4>(H, wp, bias, act, G, wave, lane); break;
-        case 3: run_layer<3>(H, wp, bias, act, G, wave, lane); break;
-        case 2: run_layer<2>(H, wp, bias, act, G, wave, lane); break;
-        case 1: run_layer<1>(H, wp, bias, act, G, wave, lane); break;
-        default: __syncthreads(); break;  // idle wave still joins the barrier
+      if (NT == 1) {
+        run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid);
+      } else {
+        const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
+        switch (cnt) {
+          case 4: run_layer<MR, 4>(H, wp, bias, act, G, wave, lane); break;
+          case 3: run_layer<MR, 3>(H, wp, bias, act, G, wave, lane); break;
+          case 2: run_layer<MR, 2>(H, wp, bias, act, G, wave, lane); break;
+          case 1: run_layer<MR, 1>(H, wp, bias, act, G, wave, lane); break;
+          default: __syncthreads(); break;  // idle wave still joins the barrier
+        }
       }
       __syncthreads();
     }
     // ---- output: StandardScaler.inverse_transform (in-place fp32, fp64 ops) + FK
-    if (tid < kBM) {
+    if (tid < BM) {
       bool valid = pt < a.n;
       double err = 0.0;
       if (valid) {
@@ -217,24 +277,27 @@ __global__ __launch_bounds__(256, 1) void ann_fused_kernel(AnnArgs a) {
         }
         *reinterpret_cast<f32x4 *>(a.ang + 4 * pt) = f32x4{y[0], y[1], y[2], y[3]};
         if (a.fk_err) {
-          d3 J[4];
-          int st = fk_chain(a.r.dh, th, J);
-          d3 p = {px, py, pz};
-          err = (st == IK_OK) ? dist3(J[3], p) : __builtin_nan("");
+          err = fk_error(a.r, th, px, py, pz);
           a.fk_err[pt] = err;
         }
       }
       if (a.fk_err) {
         double e = (valid && err == err) ? err : 0.0;
-        double mx = wave_max_f64(e);
-        double sm = wave_sum_f64(e);
-        if (lane == 0) {
-          atomicMax(&a.S->max_fk_err_bits, (unsigned long long)__double_as_longlong(mx));
-          atomicAdd(&a.S->sum_fk_err, sm);
-        }
+        blk_max = fmax(blk_max, e);
+        blk_sum += e;
       }
     }
     __syncthreads();  // the next tile's staging overwrites H
+  }
+  // per-block FK-error stats: one atomic pair per wave holding points, into its shard
+  if (a.fk_err && tid < BM) {
+    double mx = wave_max_f64(blk_max);
+    double sm = wave_sum_f64(blk_sum);
+    if (lane == 0) {
+      const int sh = blockIdx.x % kStatShards;
+      atomicMax(&a.S->max_fk_err_bits[sh], (unsigned long long)__double_as_longlong(mx));
+      atomicAdd(&a.S->sum_fk_err[sh], sm);
+    }
   }
 }
 
@@ -261,6 +324,18 @@ void ann_pack_layer(const float *W, int k, int n, float *dst) {
         }
 }
 
+static int ann_tile_rows() {
+  static int mr = 0;
+  if (mr == 0) {
+    // MR = 2 measured faster on MI355X (1M points, 3-12x500-4): 44.9 ms vs 49.0 ms
+    // (tools/sweep_ann.py): the halved weight reuse of MR = 1 costs more than
+    // the epilogue overlap it buys.
+    const char *v = getenv("IKHIP_ANN_MR");
+    mr = (v && atoi(v) == 1) ? 1 : 2;
+  }
+  return mr;
+}
+
 void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
                 float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st) {
   if (n <= 0) return;
@@ -278,10 +353,16 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  int64_t ntiles = (n + kBM - 1) / kBM;
-  unsigned grid = (unsigned)(ntiles < cus ? ntiles : cus);
+  const int mr = ann_tile_rows();
+  const int64_t bm = 32 * mr;
+  const int64_t ntiles = (n + bm - 1) / bm;
+  const int64_t slots = (int64_t)cus * (mr == 2 ? 1 : 2);  // resident workgroups
+  unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);
   kt_begin("ann_fused_kernel", st);
-  hipLaunchKernelGGL(ann_fused_kernel, dim3(grid), dim3(256), 0, st, a);
+  if (mr == 2)
+    hipLaunchKernelGGL(ann_fused_kernel<2>, dim3(grid), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(ann_fused_kernel<1>, dim3(grid), dim3(256), 0, st, a);
   kt_end(st);
 }
 

@@ -116,13 +116,20 @@ void stats_from_dev(const DevStats &d, ik_stats *s) {
     s->first_err = (int64_t)(d.first_err_key >> 8);
     s->first_err_code = (int32_t)(d.first_err_key & 0xff);
   }
-  s->max_iters = d.max_iters;
-  s->sum_iters = (int64_t)d.sum_iters;
-  s->n_capped = (int64_t)d.n_capped;
-  double mx;
-  std::memcpy(&mx, &d.max_fk_err_bits, sizeof(mx));
-  s->max_fk_err = mx;
-  s->sum_fk_err = d.sum_fk_err;
+  s->max_iters = 0;
+  s->sum_iters = 0;
+  s->n_capped = 0;
+  s->max_fk_err = 0.0;
+  s->sum_fk_err = 0.0;
+  for (int i = 0; i < kStatShards; ++i) {
+    s->max_iters = d.max_iters[i] > s->max_iters ? d.max_iters[i] : s->max_iters;
+    s->sum_iters += (int64_t)d.sum_iters[i];
+    s->n_capped += (int64_t)d.n_capped[i];
+    double mx;
+    std::memcpy(&mx, &d.max_fk_err_bits[i], sizeof(mx));
+    s->max_fk_err = mx > s->max_fk_err ? mx : s->max_fk_err;
+    s->sum_fk_err += d.sum_fk_err[i];
+  }
 }
 
 int finish(ik_ctx *c, int flags, ik_stats *stats) {

@@ -18,17 +18,21 @@ namespace ikhip {
 
 constexpr double kPi = 3.141592653589793;  // math.pi
 
-// Device-side accumulators of one call (reset by reset_stats_kernel).
+// Device-side accumulators of one call (reset by reset_stats_kernel).  The
+// batch sums are sharded: each workgroup reduces in registers/LDS and adds to
+// shard blockIdx % kStatShards, so no single word takes more than a few
+// hundred atomics per launch; the host folds the shards.
+constexpr int kStatShards = 64;
 struct DevStats {
   unsigned long long first_oob;      // atomicMin of point index
   unsigned long long first_err_key;  // atomicMin of (index << 8) | code
-  unsigned long long sum_iters;
-  unsigned long long n_capped;
-  unsigned long long max_fk_err_bits;  // atomicMax on the bits of a non-negative double
-  double sum_fk_err;
-  int max_iters;
-  int pad0;
-  unsigned long long queue;  // work-queue head (persistent kernels)
+  unsigned long long queue;          // work-queue head (persistent kernels)
+  unsigned long long pad0;
+  unsigned long long sum_iters[kStatShards];
+  unsigned long long n_capped[kStatShards];
+  unsigned long long max_fk_err_bits[kStatShards];  // atomicMax on non-negative double bits
+  double sum_fk_err[kStatShards];
+  int max_iters[kStatShards];
 };
 
 struct d3 {
@@ -204,6 +208,38 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// Block-wide FABRIK iteration stats (blockDim 256): one atomic per counter per
+// block, into the block's shard.  Every thread of the block must call it.
+__device__ __forceinline__ void block_iter_stats(DevStats *S, bool valid, int it, int max_iter) {
+  __shared__ unsigned long long red_s[4], red_c[4];
+  __shared__ int red_m[4];
+  unsigned long long s = valid ? (unsigned long long)it : 0ull;
+  unsigned long long c = (valid && it >= max_iter) ? 1ull : 0ull;
+  int m = valid ? it : 0;
+  s = wave_sum_u64(s);
+  c = wave_sum_u64(c);
+  m = wave_max_i32(m);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red_s[w] = s;
+    red_c[w] = c;
+    red_m[w] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (blockDim.x + 63) >> 6;
+    for (int i = 1; i < nw; ++i) {
+      s += red_s[i];
+      c += red_c[i];
+      m = max(m, red_m[i]);
+    }
+    const int sh = blockIdx.x % kStatShards;
+    if (s) atomicAdd(&S->sum_iters[sh], s);
+    if (c) atomicAdd(&S->n_capped[sh], c);
+    if (m) atomicMax(&S->max_iters[sh], m);
+  }
 }
 
 }  // namespace ikhip

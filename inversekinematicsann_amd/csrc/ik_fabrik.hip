@@ -85,20 +85,6 @@ __device__ __forceinline__ void load_joints(const double *src, int64_t i, d3 J[4
   J[3] = {v4.y, v5.x, v5.y};
 }
 
-// Per-wave FABRIK stats -> one atomic each per wave.
-__device__ __forceinline__ void wave_iter_stats(DevStats *S, bool valid, int it, int max_iter) {
-  unsigned long long s = valid ? (unsigned long long)it : 0ull;
-  unsigned long long c = (valid && it >= max_iter) ? 1ull : 0ull;
-  int m = valid ? it : 0;
-  s = wave_sum_u64(s);
-  c = wave_sum_u64(c);
-  m = wave_max_i32(m);
-  if ((threadIdx.x & 63) == 0) {
-    if (s) atomicAdd(&S->sum_iters, s);
-    if (c) atomicAdd(&S->n_capped, c);
-    if (m) atomicMax(&S->max_iters, m);
-  }
-}
 
 struct FabArgs {
   RobotDev r;
@@ -113,7 +99,13 @@ struct FabArgs {
   double *seeds;   // split pipeline scratch (n x 12)
   uint8_t *status; // split pipeline scratch (n)
   DevStats *S;
+  int chunk;       // work-queue grab size of the persistent iteration kernel
 };
+
+static int env_int(const char *name, int dflt) {
+  const char *v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
 
 // ------------------------------------------------------------- simple ----
 __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
@@ -143,7 +135,7 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
     if (a.iters) a.iters[i] = it;
     if (a.joints) store_joints(a.joints, i, J);
   }
-  wave_iter_stats(a.S, valid, it, a.max_iter);
+  block_iter_stats(a.S, valid, it, a.max_iter);
 }
 
 // -------------------------------------------------------------- split ----
@@ -161,7 +153,8 @@ __global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a) {
 }
 
 // 2. persistent iteration with per-lane refill.
-constexpr int kQueueChunk = 512;  // points a wave takes from the global queue at once
+// a.chunk: points a wave takes from the global queue at once (tuning knob,
+// IKHIP_FABRIK_CHUNK; small enough that every wave gets work at 1M points).
 
 template <int REFILL_MIN>
 __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
@@ -190,14 +183,14 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
       while (handed < nfree) {
         if (qnext >= qend) {
           unsigned long long old = 0;
-          if (lane == 0) old = atomicAdd(&a.S->queue, (unsigned long long)kQueueChunk);
+          if (lane == 0) old = atomicAdd(&a.S->queue, (unsigned long long)a.chunk);
           old = __shfl(old, 0, 64);
           if ((int64_t)old >= a.n) {
             exhausted = true;
             break;
           }
           qnext = (int64_t)old;
-          qend = min((int64_t)old + kQueueChunk, a.n);
+          qend = min((int64_t)old + a.chunk, a.n);
         }
         int take = (int)min((int64_t)(nfree - handed), qend - qnext);
         if (!active && rank >= handed && rank < handed + take) mine = qnext + (rank - handed);
@@ -251,7 +244,7 @@ __global__ __launch_bounds__(256) void fabrik_angles_kernel(FabArgs a) {
     o[0] = make_double2(th[0], th[1]);
     o[1] = make_double2(th[2], th[3]);
   }
-  wave_iter_stats(a.S, valid, it, a.max_iter);
+  block_iter_stats(a.S, valid, it, a.max_iter);
 }
 
 size_t fabrik_scratch_bytes(int64_t n) {
@@ -292,6 +285,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   a.iters = iters;
   a.joints = joints;
   a.S = S;
+  a.chunk = 64;
   unsigned grid = (unsigned)((n + 255) / 256);
   if (variant == 0) {
     a.seeds = nullptr;
@@ -314,7 +308,14 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   kt_begin("fabrik_seed_kernel", stream);
   hipLaunchKernelGGL(fabrik_seed_kernel, dim3(grid), dim3(256), 0, stream, a);
   kt_end(stream);
-  unsigned pgrid = (unsigned)num_cus() * 8;
+  // persistent grid: blocks_per_cu 256-thread blocks per CU (= waves per SIMD)
+  // measured on MI355X at 1M points (tools/sweep_fabrik.py): 2 blocks/CU with
+  // 64-point grabs beats 4 and 8 (more lanes = fewer points per lane = a
+  // longer divergent tail) by 10-30 %.
+  static const int bpc = env_int("IKHIP_FABRIK_BPC", 2);
+  static const int chunk = env_int("IKHIP_FABRIK_CHUNK", 64);
+  a.chunk = chunk > 0 ? chunk : 64;
+  unsigned pgrid = (unsigned)num_cus() * (unsigned)(bpc > 0 ? bpc : 8);
   int64_t waves_needed = (n + 63) / 64;
   if ((int64_t)pgrid * 4 > waves_needed)
     pgrid = (unsigned)((waves_needed + 3) / 4 > 0 ? (waves_needed + 3) / 4 : 1);
@@ -374,7 +375,7 @@ __global__ __launch_bounds__(256) void fabrik_calc_kernel(const double *dists_in
     }
     if (iters) iters[i] = it;
   }
-  wave_iter_stats(S, valid, it, max_iter);
+  block_iter_stats(S, valid, it, max_iter);
 }
 
 void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,

@@ -8,16 +8,19 @@
 namespace ikhip {
 
 __global__ void reset_stats_kernel(DevStats *S) {
-  if (threadIdx.x == 0) {
+  const int t = threadIdx.x;
+  if (t == 0) {
     S->first_oob = ~0ull;
     S->first_err_key = ~0ull;
-    S->sum_iters = 0;
-    S->n_capped = 0;
-    S->max_fk_err_bits = 0;
-    S->sum_fk_err = 0.0;
-    S->max_iters = 0;
-    S->pad0 = 0;
     S->queue = 0;
+    S->pad0 = 0;
+  }
+  if (t < kStatShards) {
+    S->sum_iters[t] = 0;
+    S->n_capped[t] = 0;
+    S->max_fk_err_bits[t] = 0;
+    S->sum_fk_err[t] = 0.0;
+    S->max_iters[t] = 0;
   }
 }
 

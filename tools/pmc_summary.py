@@ -1,0 +1,38 @@
+"""Per-kernel averages of every PMC counter found under the given rocprofv3
+--pmc output directories (counter_collection.csv), plus derived ratios.
+
+    python tools/pmc_summary.py DIR [DIR ...]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def main(dirs):
+    tot = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(lambda: defaultdict(set))
+    for d in dirs:
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    name = row.get("Kernel_Name", "")
+                    short = name.split("(")[0].split("::")[-1]
+                    c = row["Counter_Name"]
+                    tot[short][c] += float(row["Counter_Value"])
+                    disp[short][c].add(row.get("Dispatch_Id"))
+    out = {}
+    for k, cs in tot.items():
+        avg = {c: v / max(1, len(disp[k][c])) for c, v in cs.items()}
+        if "GRBM_GUI_ACTIVE" in avg and "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+            avg["MfmaUtil_pct"] = 100 * avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] * 1024)
+        if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
+            avg["L2_hit_pct"] = 100 * avg["TCC_HIT_sum"] / max(1, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
+        out[k] = avg
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,49 @@
+"""Time the FABRIK pipeline under different persistent-grid settings.
+Each setting runs in a fresh subprocess (the knobs are read once per process)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CODE = r'''
+import sys, json, torch, numpy as np
+sys.path.insert(0, %r)
+from inversekinematicsann_amd import _native
+from inversekinematicsann_amd.robot.position_generator import random_dist
+n = int(sys.argv[1]); tol = float(sys.argv[2]); mi = int(sys.argv[3])
+pts = torch.from_numpy(random_dist(n, seed=0)).cuda()
+ang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
+it = torch.empty(n, dtype=torch.int32, device="cuda")
+ctx = _native.Context(0)
+F = _native.IK_F_DEVICE
+for _ in range(3): ctx.fabrik_solve_device(pts, ang, it, None, tol, mi, flags=F)
+ctx.set_timing(True)
+res = {}
+for _ in range(5):
+    ctx.fabrik_solve_device(pts, ang, it, None, tol, mi, flags=F)
+    for k, v in ctx.kernel_times():
+        res.setdefault(k, []).append(v)
+print(json.dumps({k: min(v) for k, v in res.items()}))
+''' % ROOT
+
+def run(env, n, tol, mi):
+    e = dict(os.environ); e.update(env)
+    out = subprocess.run([sys.executable, "-c", CODE, str(n), str(tol), str(mi)], env=e,
+                         capture_output=True, text=True, timeout=300)
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    return json.loads(line[-1]) if line else {"error": out.stderr[-500:]}
+
+if __name__ == "__main__":
+    cases = []
+    for var in ("1", "2", "0"):
+        for bpc in ("2", "4", "8"):
+            for chunk in ("64", "256"):
+                if var == "0" and (bpc != "8" or chunk != "64"):
+                    continue
+                cases.append({"IKHIP_FABRIK_VARIANT": var, "IKHIP_FABRIK_BPC": bpc,
+                              "IKHIP_FABRIK_CHUNK": chunk})
+    for n, tol, mi in ((1_000_000, 1e-3, 100), (1_000_000, 1e-5, 200)):
+        for c in cases:
+            r = run(c, n, tol, mi)
+            print(json.dumps({"n": n, "tol": tol, **c, **r}), flush=True)
