@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--secondary", type=int, default=1,
                     help="also time the other method and report it under 'secondary'")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--gather", type=int, default=0,
+                    help="N>1: include the RCCL all_gather of every rank's angle rows in the "
+                         "timed step (delivers the whole batch to every rank)")
     return ap.parse_args()
 
 
@@ -101,6 +104,20 @@ def load_traffic(path, kernel):
         return None
 
 
+def make_gather(dang, args, world):
+    """The optional delivery step: all_gather of the per-rank angle rows over
+    RCCL (inversekinematicsann_amd.dist.gather_rows), on the solve's stream."""
+    if not args.gather or world == 1:
+        return lambda: None
+    from inversekinematicsann_amd.dist import gather_rows
+    n_total = dang.shape[0] * world
+
+    def gather():
+        gather_rows(dang, n_total)
+
+    return gather
+
+
 def run_ann(ctx, dpts, n, args, world):
     import torch
     from inversekinematicsann_amd import _native
@@ -112,8 +129,11 @@ def run_ann(ctx, dpts, n, args, world):
     derr = torch.empty(n, dtype=torch.float64, device="cuda")
     flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
 
+    gather = make_gather(dang, args, world)
+
     def step():
         ctx.ann_solve_device(dpts, dang, derr, flags=flags)
+        gather()
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
@@ -142,8 +162,11 @@ def run_fabrik(ctx, dpts, n, args, world):
     dit = torch.empty(n, dtype=torch.int32, device="cuda")
     flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
 
+    gather = make_gather(dang, args, world)
+
     def step():
         ctx.fabrik_solve_device(dpts, dang, dit, None, args.tol, args.max_iter, flags=flags)
+        gather()
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
@@ -252,7 +275,10 @@ def main():
     pts = random_dist(n, seed=rank)  # rank r solves shard r of the N x 1M global batch
     dpts = torch.from_numpy(pts).cuda()
     ctx = _native.Context(local)
-    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    # one non-default stream shared by the library, torch events and collectives
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
     runners = {"ann": run_ann, "fabrik": run_fabrik}
     res = runners[args.method](ctx, dpts, n, args, world)
     secondary = {}
@@ -276,6 +302,7 @@ def main():
                 "(the reference .h5 is not shipped); reference StandardScaler constants",
         "config": {"workload": res["workload"], "points_per_gpu": n, "total_points": total,
                    "parallelism": f"dp{world}", "method": args.method,
+                   "all_gather_in_step": bool(args.gather and world > 1),
                    "tol": args.tol if args.method == "fabrik" else None,
                    "max_iter": args.max_iter if args.method == "fabrik" else None},
         "roofline": res["roofline"],

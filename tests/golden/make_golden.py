@@ -221,3 +221,60 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+# --------------------------------------------------------------------- CLI ----
+_CLI_WRAPPER = r'''
+import runpy, sys, types
+keras = types.ModuleType("keras")
+for sub, names in {"models": ["load_model", "Sequential"], "optimizers": ["Adam"],
+                   "layers": ["Dense", "Input"], "callbacks": ["EarlyStopping"]}.items():
+    m = types.ModuleType("keras." + sub)
+    for n in names:
+        setattr(m, n, None)
+    sys.modules["keras." + sub] = m
+    setattr(keras, sub, m)
+keras.activations = types.SimpleNamespace(tanh=None)
+sys.modules["keras"] = keras
+sys.path.insert(0, "/root/reference")
+sys.argv = ["cli.py"] + sys.argv[1:]
+runpy.run_path("/root/reference/cli.py", run_name="__main__")
+'''
+
+
+def cli_goldens():
+    """Run the reference CLI (FABRIK method) on two CSVs; record stdout, exit
+    code and the output CSV text."""
+    import subprocess
+    import tempfile
+    tmp = tempfile.mkdtemp()
+    wrapper = os.path.join(tmp, "run_ref_cli.py")
+    with open(wrapper, "w") as f:
+        f.write(_CLI_WRAPPER)
+    spring_csv = os.path.join(OUT, "cli_spring20_points.csv")
+    oor_csv = os.path.join(OUT, "cli_out_of_reach_points.csv")
+    import pandas as pd
+    pd.DataFrame(pg.TrainingDataGenerator.spring(20, 2, 3, 6),
+                 columns=["x", "y", "z"]).to_csv(spring_csv, index=False)
+    pd.DataFrame([[1.0, 2.1, 3.0], [1.567, 2.22, -3.123]],
+                 columns=["x", "y", "z"]).to_csv(oor_csv, index=False)
+    env = dict(os.environ, MPLBACKEND="Agg")
+    rec = {}
+    for name, csvp in (("spring20", spring_csv), ("out_of_reach", oor_csv)):
+        outp = os.path.join(tmp, name + "_angles.csv")
+        r = subprocess.run([sys.executable, wrapper, "--inverse-kine", "--method", "fabrik",
+                            "--points", csvp, "--to-file", outp], cwd="/root/reference",
+                           env=env, capture_output=True, text=True)
+        rec[name] = {"returncode": r.returncode, "stdout": r.stdout,
+                     "angles_csv": open(outp).read() if os.path.exists(outp) else None}
+    r = subprocess.run([sys.executable, wrapper, "--inverse-kine", "--method", "fabrik",
+                        "--example"], cwd="/root/reference", env=env, capture_output=True,
+                       text=True)
+    rec["example"] = {"returncode": r.returncode, "stdout": r.stdout}
+    with open(os.path.join(OUT, "cli_fabrik.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    print("cli_fabrik.json:", {k: v["returncode"] for k, v in rec.items()})
+
+
+if __name__ == "__main__" and "--cli" in sys.argv:
+    cli_goldens()
