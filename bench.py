@@ -61,20 +61,25 @@ def dist_setup(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    if world > 1:
+    if "WORLD_SIZE" in os.environ:  # launched by torch.distributed.run (any N)
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
+def _dist_on():
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
 def barrier(world):
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.barrier()
 
 
 def max_over_ranks(v: float, world: int) -> float:
-    if world == 1:
+    if not _dist_on():
         return v
     import torch
     import torch.distributed as dist
@@ -84,7 +89,7 @@ def max_over_ranks(v: float, world: int) -> float:
 
 
 def sum_over_ranks(v: float, world: int) -> float:
-    if world == 1:
+    if not _dist_on():
         return v
     import torch
     import torch.distributed as dist
@@ -321,7 +326,7 @@ def main():
             line["secondary"][other]["cpu_baseline"] = cpu_baseline(other, args)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if _dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
 
