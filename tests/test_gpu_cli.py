@@ -72,3 +72,28 @@ def test_cli_ann_npz_model_and_verbose(tmp_path, capsys):
                         REFERENCE_Y_SCALER.scale)
     got = pd.read_csv(out).values
     assert np.abs(got - ref).max() <= 1e-5
+
+
+def test_cli_ann_keras_h5_model(tmp_path, capsys):
+    """`--method ann --model M.h5` with M_scaler_{x,y}.bin beside it (cli.py:238-246,
+    ann.py:78-85): the Keras file is read without h5py, the scalers without unpickling."""
+    import shutil
+    import pandas as pd
+    from inversekinematicsann_amd.cli import main
+    from inversekinematicsann_amd.models.keras_h5 import load_keras_dense_model
+    from inversekinematicsann_amd.models.scaler_bin import load_scaler
+    from oracle import oracle as O
+    base = str(tmp_path / "roboarm_model")
+    shutil.copy(os.path.join(GOLDEN, "keras_dense_deep.h5"), base + ".h5")
+    for s in "xy":
+        shutil.copy(os.path.join(GOLDEN, f"roboarm_model_1674153800-982793_scaler_{s}.bin"),
+                    f"{base}_scaler_{s}.bin")
+    out = tmp_path / "ann.csv"
+    pts_csv = os.path.join(GOLDEN, "cli_spring20_points.csv")
+    assert main(["--inverse-kine", "--method", "ann", "--model", base + ".h5", "--points",
+                 pts_csv, "--to-file", str(out)]) == 0
+    m = load_keras_dense_model(base + ".h5")
+    xs, ys = load_scaler(base + "_scaler_x.bin"), load_scaler(base + "_scaler_y.bin")
+    ref = O.ann_forward(pd.read_csv(pts_csv).values, m.weights, m.biases, m.activations,
+                        xs.mean, xs.scale, ys.mean, ys.scale)
+    assert np.abs(pd.read_csv(out).values - ref).max() <= 1e-5
