@@ -131,6 +131,14 @@ int ik_ann_solve(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *
 int ik_ctx_set_timing(ik_ctx *ctx, int on);
 int ik_kernel_times(ik_ctx *ctx, int max, float *ms, char *names, int name_len);
 
+/* Diagnostics: when on, the ANN kernel's workgroup 0 records s_memtime stamps
+ * (shader clock ticks) per wave for its first 4 tiles: 32 slots per
+ * (tile, wave) -- 0 tile start, 1 input staged, 2+2l layer l GEMM done,
+ * 3+2l layer l done, 31 tile done.  ik_debug_read copies them out (returns the
+ * count, or -ik_status). */
+int ik_ctx_set_debug(ik_ctx *ctx, int on);
+int ik_debug_read(ik_ctx *ctx, uint64_t *out, int max);
+
 /* After IK_F_ASYNC calls: wait for the stream and read the accumulated stats
  * of the last call. */
 int ik_stats_fetch(ik_ctx *ctx, ik_stats *stats);

@@ -17,7 +17,9 @@ from typing import Optional, Sequence
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libikhip.so")
+# IKHIP_LIB selects another build of the same ABI (e.g. libikhip_diag.so, the
+# diagnostic build with in-kernel stamps); the default is the production build.
+LIB_PATH = os.environ.get("IKHIP_LIB") or os.path.join(_PKG, "libikhip.so")
 
 IK_OK, IK_E_OUT_OF_REACH, IK_E_DOMAIN, IK_E_ZERODIV, IK_E_ANGLE_RANGE = 0, 1, 2, 3, 4
 IK_E_BADARG, IK_E_HIP, IK_E_NOMODEL = 16, 17, 18
@@ -27,7 +29,8 @@ ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
 EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_ctx_get_stream",
                     "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk",
                     "ik_fabrik_solve", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
-                    "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times")
+                    "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
+                    "ik_ctx_set_debug", "ik_debug_read")
 
 
 class NativeUnavailable(RuntimeError):
@@ -94,6 +97,8 @@ def load_library(path: str = LIB_PATH):
         L.ik_stats_fetch.argtypes = [vp, st]
         L.ik_ctx_set_timing.argtypes = [vp, ctypes.c_int]
         L.ik_kernel_times.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int]
+        L.ik_ctx_set_debug.argtypes = [vp, ctypes.c_int]
+        L.ik_debug_read.argtypes = [vp, vp, ctypes.c_int]
         _lib = L
         return L
 
@@ -272,6 +277,17 @@ class Context:
         raw = names.raw
         return [(raw[i * 48:(i + 1) * 48].split(b"\0")[0].decode(), float(ms[i]))
                 for i in range(n)]
+
+    def set_debug(self, on: bool = True):
+        self._check(self.lib.ik_ctx_set_debug(self.handle, 1 if on else 0))
+
+    def debug_stamps(self) -> np.ndarray:
+        """ANN diagnostic stamps as (tile, wave, slot) uint64 (see ikhip.h)."""
+        out = np.zeros(4 * 4 * 32, np.uint64)
+        n = self.lib.ik_debug_read(self.handle, out.ctypes.data, out.size)
+        if n < 0:
+            raise NativeError(-n, self.lib.ik_last_error().decode())
+        return out[:n].reshape(4, 4, 32) if n == out.size else out[:n]
 
     def stats_fetch(self) -> IkStats:
         s = IkStats()

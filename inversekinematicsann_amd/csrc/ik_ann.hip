@@ -20,6 +20,8 @@
 //   MR = 1: 32-point tiles, 64.5 KiB LDS, two workgroups per CU, so one
 //           workgroup's barrier / epilogue overlaps the other's MFMAs.
 // The grid is persistent: workgroups walk the point tiles.
+#include <cmath>
+
 #include "ik_common.h"
 
 namespace ikhip {
@@ -39,22 +41,64 @@ struct AnnArgs {
   double *fk_err;
   int check_limits;
   DevStats *S;
+  unsigned long long *dbg;  // diagnostic s_memtime stamps (ik_ctx_set_debug), normally null
+  double jc[16];            // per joint {a, d, cos alpha, sin alpha} for the FK round trip
+  int alpha_bad;            // some |alpha| > 2 pi: FK raises for every point (forward.py:23-25)
 };
 
-// tanh(x) = sign(x) (1 - e) / (1 + e), e = exp(-2|x|), with the hardware
-// exp2 / reciprocal (1 ulp each): absolute error ~1e-7.
+constexpr int kStampSlots = 32;  // per (tile, wave): see ann_fused_kernel
+constexpr int kStampTiles = 4;
+// Stamps exist only in the diagnostic build (-DIKHIP_DIAG, libikhip_diag.so):
+// their pointers cost registers the production main loop does not have.
+__device__ __forceinline__ void stamp(unsigned long long *p) {
+#ifdef IKHIP_DIAG
+  if (p) *p = __builtin_amdgcn_s_memtime();
+#else
+  (void)p;
+#endif
+}
+
+// Activations with the hardware exp2 / reciprocal (1 ulp each); tanh has an
+// absolute error of ~1e-7.
 template <int ACT>
 __device__ __forceinline__ float act_apply(float v) {
   if constexpr (ACT == IK_ACT_TANH) {
-    float e = __builtin_amdgcn_exp2f(-2.885390081777927f * fabsf(v));  // exp(-2|v|)
-    float t = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
-    return copysignf(t, v);
+    // sign(v) (1 - e) / (1 + e), e = exp(-2|v|); NaN propagates
+    const float e = __builtin_amdgcn_exp2f(-fabsf(2.885390081777927f * v));
+    return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), v);
   } else if constexpr (ACT == IK_ACT_RELU) {
     return fmaxf(v, 0.0f);
   } else if constexpr (ACT == IK_ACT_SIGMOID) {
     return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
   } else {
     return v;
+  }
+}
+
+// Two elements at once: the adds / multiplies become packed-fp32 instructions
+// (v_pk_mul_f32 / v_pk_add_f32) and the two independent chains interleave, so
+// the epilogue issues ~5 instructions per element.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <int ACT>
+__device__ __forceinline__ f32x2 act_apply2(f32x2 v) {
+  if constexpr (ACT == IK_ACT_TANH) {
+    const f32x2 u = v * 2.885390081777927f;
+    f32x2 e;
+    e.x = __builtin_amdgcn_exp2f(-fabsf(u.x));
+    e.y = __builtin_amdgcn_exp2f(-fabsf(u.y));
+    const f32x2 n = 1.0f - e, d = 1.0f + e;
+    f32x2 r;
+    r.x = __builtin_amdgcn_rcpf(d.x);
+    r.y = __builtin_amdgcn_rcpf(d.y);
+    f32x2 t = n * r;
+    t.x = copysignf(t.x, v.x);
+    t.y = copysignf(t.y, v.y);
+    return t;
+  } else {
+    f32x2 t;
+    t.x = act_apply<ACT>(v.x);
+    t.y = act_apply<ACT>(v.y);
+    return t;
   }
 }
 
@@ -132,8 +176,10 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
 // C/D map of the 32x32 MFMA: column lane & 31, row (q & 3) + 8 (q >> 2) + 4 (lane >> 5).
 template <int MR, int NR, int ACT>
 __device__ __forceinline__ void layer_store(float *H, const float *__restrict__ bias, int wave,
-                                            int lane, f32x16 (&acc)[MR][NR]) {
+                                            int lane, f32x16 (&acc)[MR][NR],
+                                            unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
+  stamp(st);
   __syncthreads();  // every wave has finished reading the layer input
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
@@ -142,23 +188,28 @@ __device__ __forceinline__ void layer_store(float *H, const float *__restrict__ 
 #pragma unroll
     for (int m = 0; m < MR; ++m)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        H[row * kLd + col] = act_apply<ACT>(acc[m][j][q] + bv);
+      for (int q = 0; q < 16; q += 2) {
+        const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;  // row of q + 1 is row + 1
+        const f32x2 t = act_apply2<ACT>(f32x2{acc[m][j][q], acc[m][j][q + 1]} + bv);
+        H[row * kLd + col] = t.x;
+        H[(row + 1) * kLd + col] = t.y;
       }
   }
 }
 
+// One Dense layer for a wave with NR column tiles (bias in the accumulator).
 template <int MR, int NR>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
-                                          int G, int wave, int lane) {
+                                          int G, int wave, int lane, unsigned long long *st) {
   f32x16 acc[MR][NR];
   layer_gemm<MR, NR>(H, wp, G, 0, G, wave, kWaves, lane, acc);
   switch (act) {
-    case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bias, wave, lane, acc); break;
-    case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bias, wave, lane, acc); break;
-    case IK_ACT_SIGMOID: layer_store<MR, NR, IK_ACT_SIGMOID>(H, bias, wave, lane, acc); break;
-    default: layer_store<MR, NR, IK_ACT_LINEAR>(H, bias, wave, lane, acc); break;
+    case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bias, wave, lane, acc, st); break;
+    case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bias, wave, lane, acc, st); break;
+    case IK_ACT_SIGMOID:
+      layer_store<MR, NR, IK_ACT_SIGMOID>(H, bias, wave, lane, acc, st);
+      break;
+    default: layer_store<MR, NR, IK_ACT_LINEAR>(H, bias, wave, lane, acc, st); break;
   }
 }
 
@@ -178,11 +229,13 @@ __device__ __forceinline__ void splitk_finish(float *H, const float *__restrict_
 // summed in a fixed order, so no wave idles.
 template <int MR>
 __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, const float *bias,
-                                                 int act, int G, int wave, int lane, int tid) {
+                                                 int act, int G, int wave, int lane, int tid,
+                                                 unsigned long long *st) {
   constexpr int BM = 32 * MR;
   f32x16 acc[MR][1];
   const int g0 = (G * wave) / kWaves, g1 = (G * (wave + 1)) / kWaves;
   layer_gemm<MR, 1>(H, wp, G, g0, g1, 0, 0, lane, acc);
+  stamp(st);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
@@ -201,13 +254,33 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
   }
 }
 
-// The FK round trip of one point (cli.py:54-61 + the distance to the target).
-__device__ __forceinline__ double fk_error(const RobotDev &r, const double th[4],
-                                                     double px, double py, double pz) {
-  d3 J[4];
-  int st = fk_chain(r.dh, th, J);
-  d3 p = {px, py, pz};
-  return (st == IK_OK) ? dist3(J[3], p) : __builtin_nan("");
+// The FK round trip of one point (cli.py:54-61 + the distance to the target),
+// register-lean: the effector is Rz(t1) B1 Rz(t2) B2 Rz(t3) B3 Rz(t4) B4 e4
+// with B_i = Tz(d_i) Tx(a_i) Rx(alpha_i) (forward.py:63-70 regrouped),
+// applied right to left to a vector; jc[i] = {a_i, d_i, cos alpha_i, sin alpha_i}
+// from the host.  Same value as fk_chain up to rounding (~1e-15).
+__device__ __forceinline__ double fk_error(const double *jc, const double th[4], double px,
+                                           double py, double pz, int alpha_bad) {
+  bool ok = !alpha_bad;
+  double x = jc[12], y = 0.0, z = jc[13];  // B4 e4 = (a4, 0, d4)
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    ok = ok && angle_ok(th[i]);
+    double s, c;
+    sincos(th[i], &s, &c);
+    double xr = c * x - s * y, yr = s * x + c * y;  // Rz(t_i)
+    x = xr;
+    y = yr;
+    if (i > 0) {  // B_{i} (1-based), i.e. jc[i - 1]
+      const double *b = jc + 4 * (i - 1);
+      double yb = b[2] * y - b[3] * z, zb = b[3] * y + b[2] * z + b[1];
+      x = x + b[0];
+      y = yb;
+      z = zb;
+    }
+  }
+  d3 e = {x, y, z}, p = {px, py, pz};
+  return ok ? dist3(e, p) : __builtin_nan("");
 }
 
 template <int MR>
@@ -221,6 +294,13 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t pt = tile * BM + tid;
+    // diagnostic stamps (block 0, first tiles, lane 0 of each wave): slot 0 tile
+    // start, 1 staged, 2+2l layer l GEMM done, 3+2l layer l done, 31 tile done
+    unsigned long long *stp = nullptr;
+    const int64_t it_local = tile / gridDim.x;  // this workgroup's tile counter
+    if (a.dbg && blockIdx.x == 0 && lane == 0 && it_local < kStampTiles)
+      stp = a.dbg + ((size_t)it_local * kWaves + wave) * kStampSlots;
+    stamp(stp);
     double px = 0.0, py = 0.0, pz = 0.0;
     // ---- input: workspace check + StandardScaler.transform (float64) -> fp32
     if (tid < BM) {
@@ -240,6 +320,7 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
       row[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
     __syncthreads();
+    stamp(stp ? stp + 1 : nullptr);
     // ---- Dense layers
     for (int l = 0; l < a.m.n_layers; ++l) {
       const int G = a.m.kp[l] >> 3;
@@ -247,19 +328,21 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
       const f32x4 *wp = reinterpret_cast<const f32x4 *>(a.m.wp[l]);
       const float *bias = a.m.bias[l];
       const int act = a.m.act[l];
+      unsigned long long *sl = (stp && l < 14) ? stp + 2 + 2 * l : nullptr;
       if (NT == 1) {
-        run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid);
+        run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid, sl);
       } else {
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4>(H, wp, bias, act, G, wave, lane); break;
-          case 3: run_layer<MR, 3>(H, wp, bias, act, G, wave, lane); break;
-          case 2: run_layer<MR, 2>(H, wp, bias, act, G, wave, lane); break;
-          case 1: run_layer<MR, 1>(H, wp, bias, act, G, wave, lane); break;
+          case 4: run_layer<MR, 4>(H, wp, bias, act, G, wave, lane, sl); break;
+          case 3: run_layer<MR, 3>(H, wp, bias, act, G, wave, lane, sl); break;
+          case 2: run_layer<MR, 2>(H, wp, bias, act, G, wave, lane, sl); break;
+          case 1: run_layer<MR, 1>(H, wp, bias, act, G, wave, lane, sl); break;
           default: __syncthreads(); break;  // idle wave still joins the barrier
         }
       }
       __syncthreads();
+      stamp(sl ? sl + 1 : nullptr);
     }
     // ---- output: StandardScaler.inverse_transform (in-place fp32, fp64 ops) + FK
     if (tid < BM) {
@@ -277,7 +360,7 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
         }
         *reinterpret_cast<f32x4 *>(a.ang + 4 * pt) = f32x4{y[0], y[1], y[2], y[3]};
         if (a.fk_err) {
-          err = fk_error(a.r, th, px, py, pz);
+          err = fk_error(a.jc, th, px, py, pz, a.alpha_bad);
           a.fk_err[pt] = err;
         }
       }
@@ -288,6 +371,7 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
       }
     }
     __syncthreads();  // the next tile's staging overwrites H
+    stamp(stp ? stp + kStampSlots - 1 : nullptr);
   }
   // per-block FK-error stats: one atomic pair per wave holding points, into its shard
   if (a.fk_err && tid < BM) {
@@ -336,8 +420,11 @@ static int ann_tile_rows() {
   return mr;
 }
 
+size_t ann_debug_words() { return (size_t)kStampTiles * kWaves * kStampSlots; }
+
 void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
-                float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st) {
+                float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
+                unsigned long long *dbg) {
   if (n <= 0) return;
   AnnArgs a;
   a.m = m;
@@ -348,6 +435,16 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   a.fk_err = fk_err;
   a.check_limits = check_limits ? 1 : 0;
   a.S = S;
+  a.dbg = dbg;
+  a.alpha_bad = 0;
+  for (int i = 0; i < 4; ++i) {
+    const double al = r.dh[12 + i];
+    a.jc[4 * i + 0] = r.dh[8 + i];  // a_i
+    a.jc[4 * i + 1] = r.dh[4 + i];  // d_i
+    a.jc[4 * i + 2] = std::cos(al);
+    a.jc[4 * i + 3] = std::sin(al);
+    if (al < -2 * kPi || al > 2 * kPi) a.alpha_bad = 1;
+  }
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

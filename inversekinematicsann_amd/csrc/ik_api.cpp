@@ -78,6 +78,7 @@ struct ik_ctx {
   void *ann_buf = nullptr;
   int fabrik_variant = 1;
   KTimer kt;
+  unsigned long long *dbg = nullptr;  // diagnostic stamp buffer (ik_ctx_set_debug)
 };
 
 namespace {
@@ -203,6 +204,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->ann_buf) (void)hipFree(c->ann_buf);
   if (c->d_stats) (void)hipFree(c->d_stats);
+  if (c->dbg) (void)hipFree(c->dbg);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   for (int i = 0; i < kMaxTimed; ++i) {
@@ -259,6 +261,32 @@ int ik_kernel_times(ik_ctx *c, int max, float *ms, char *names, int name_len) {
       names[(size_t)i * name_len + name_len - 1] = 0;
     }
   }
+  return n;
+}
+
+int ik_ctx_set_debug(ik_ctx *c, int on) {
+  if (!c) return fail(IK_E_BADARG, "ik_ctx_set_debug: NULL context");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  IK_HIP(hipStreamSynchronize(c->stream));
+  if (on && !c->dbg) {
+    IK_HIP(hipMalloc(&c->dbg, ann_debug_words() * 8));
+    IK_HIP(hipMemset(c->dbg, 0, ann_debug_words() * 8));
+  } else if (!on && c->dbg) {
+    IK_HIP(hipFree(c->dbg));
+    c->dbg = nullptr;
+  }
+  return IK_OK;
+}
+
+int ik_debug_read(ik_ctx *c, uint64_t *out, int max) {
+  if (!c || !out || max < 0) return -IK_E_BADARG;
+  if (!c->dbg) return 0;
+  if (set_dev(c)) return -IK_E_HIP;
+  int n = (int)ann_debug_words() < max ? (int)ann_debug_words() : max;
+  if (hipStreamSynchronize(c->stream) != hipSuccess) return -IK_E_HIP;
+  if (hipMemcpy(out, c->dbg, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return -IK_E_HIP;
   return n;
 }
 
@@ -506,7 +534,8 @@ int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk
     de = fk_err ? reinterpret_cast<double *>(s + b_in + b_a) : nullptr;
   }
   launch_reset_stats(c->d_stats, c->stream);
-  launch_ann(c->ann, c->robot, dp, n, da, de, !(flags & IK_F_NO_LIMITS), c->d_stats, c->stream);
+  launch_ann(c->ann, c->robot, dp, n, da, de, !(flags & IK_F_NO_LIMITS), c->d_stats, c->stream,
+             c->dbg);
   IK_HIP(hipGetLastError());
   if (!dev && n > 0) {
     IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));

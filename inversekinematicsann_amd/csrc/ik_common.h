@@ -285,6 +285,8 @@ struct AnnModelDev {
 };
 size_t ann_packed_floats(int k, int n);  // floats of one packed layer
 void ann_pack_layer(const float *W, int k, int n, float *dst);  // host-side packing
+size_t ann_debug_words();  // u64 slots of the diagnostic stamp buffer
 void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
-                float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st);
+                float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
+                unsigned long long *dbg);
 }  // namespace ikhip
