@@ -123,6 +123,17 @@ int ik_ann_load(ik_ctx *ctx, int n_layers, const int32_t *dims, const int32_t *a
 int ik_ann_solve(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *fk_err,
                  int flags, ik_stats *stats);
 
+/* Arithmetic of the hidden-layer GEMMs.  IK_ANN_FP32 (default): fp32 MFMA
+ * (v_mfma_f32_32x32x2_f32), a fp32 dot product like the reference's TF/Keras
+ * CPU float32 forward.  IK_ANN_BF16X6: every fp32 operand split into three bf16
+ * parts and six bf16 MFMA products accumulated in fp32 -- fp32-level accuracy
+ * (tested within 1e-6 of a float64 forward, the fp32 mode's own distance from
+ * it) at ~2.7x the MFMA rate.  The input layer and a one-tile output layer stay
+ * fp32 in both modes.  Environment default: IKHIP_ANN_MODE=bf16x6. */
+enum { IK_ANN_FP32 = 0, IK_ANN_BF16X6 = 1 };
+int ik_ann_set_mode(ik_ctx *ctx, int mode);
+int ik_ann_get_mode(ik_ctx *ctx); /* the mode, or -ik_status */
+
 /* Per-kernel timing with HIP events on the context's stream: when on, every
  * kernel a call launches is bracketed by hipEventRecord.  ik_kernel_times
  * waits for the last call's events and returns how many kernels it timed,

@@ -30,7 +30,8 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk",
                     "ik_fabrik_solve", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
-                    "ik_ctx_set_debug", "ik_debug_read")
+                    "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode")
+ANN_MODES = {"fp32": 0, "bf16x6": 1}
 
 
 class NativeUnavailable(RuntimeError):
@@ -99,6 +100,8 @@ def load_library(path: str = LIB_PATH):
         L.ik_kernel_times.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int]
         L.ik_ctx_set_debug.argtypes = [vp, ctypes.c_int]
         L.ik_debug_read.argtypes = [vp, vp, ctypes.c_int]
+        L.ik_ann_set_mode.argtypes = [vp, ctypes.c_int]
+        L.ik_ann_get_mode.argtypes = [vp]
         _lib = L
         return L
 
@@ -246,6 +249,18 @@ class Context:
         sc = [_host(v, np.float64).reshape(-1) for v in (x_mean, x_scale, y_mean, y_scale)]
         self._check(self.lib.ik_ann_load(self.handle, nl, _ptr(dims_a), _ptr(acts_a), wp, bp,
                                          *[_ptr(v) for v in sc]))
+
+    def ann_set_mode(self, mode: str):
+        """Hidden-layer GEMM arithmetic: "fp32" (default) or "bf16x6" (ikhip.h)."""
+        if mode not in ANN_MODES:
+            raise ValueError(f"unknown ANN mode {mode!r}; expected one of {sorted(ANN_MODES)}")
+        self._check(self.lib.ik_ann_set_mode(self.handle, ANN_MODES[mode]))
+
+    def ann_mode(self) -> str:
+        m = self.lib.ik_ann_get_mode(self.handle)
+        if m < 0:
+            raise NativeError(-m, self.lib.ik_last_error().decode())
+        return {v: k for k, v in ANN_MODES.items()}[m]
 
     def ann_solve(self, pts, check_limits=True, want_fk_err=False):
         s = IkStats()

@@ -21,6 +21,7 @@
 //           workgroup's barrier / epilogue overlaps the other's MFMAs.
 // The grid is persistent: workgroups walk the point tiles.
 #include <cmath>
+#include <cstring>
 
 #include "ik_common.h"
 
@@ -197,12 +198,164 @@ __device__ __forceinline__ void layer_store(float *H, const float *__restrict__ 
   }
 }
 
-// One Dense layer for a wave with NR column tiles (bias in the accumulator).
+// ------------------------------------------------ split-bf16 (bf16x6) mode ----
+// Opt-in (IK_ANN_MODE_BF16X6): fp32 operands are split into three bf16 parts,
+// x = hi + mid + lo (each residual exact in fp32), and the six products whose
+// order is above 2^-24 -- lo*hi, mid*mid, hi*lo, mid*hi, hi*mid, hi*hi -- are
+// accumulated in fp32 by v_mfma_f32_32x32x16_bf16 (exact bf16 products).  The
+// result is fp32-accurate (max |d| vs a float64 forward ~1e-7 on the reference
+// architecture, tests/test_gpu_parity.py) at 6 bf16 MFMAs (192 cycles) per
+// 32x32x16 block instead of 8 fp32 ones (512 cycles).  Weights are split on
+// the host into three fragment-ordered planes; activations are split in VALU
+// as they are read from LDS, in the MFMA issue gaps.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct Split3 {
+  bf16x8 hi, mid, lo;
+};
+
+__device__ __forceinline__ Split3 split3(f32x8 x) {
+  u32x4 h, m, l;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 v = {x[2 * i], x[2 * i + 1]};
+    const uint32_t ph = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+    const f32x2 vh = {__builtin_bit_cast(float, ph << 16),
+                      __builtin_bit_cast(float, ph & 0xffff0000u)};
+    const f32x2 r1 = v - vh;
+    const uint32_t pm = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1, bf16x2));
+    const f32x2 vm = {__builtin_bit_cast(float, pm << 16),
+                      __builtin_bit_cast(float, pm & 0xffff0000u)};
+    const f32x2 r2 = r1 - vm;
+    h[i] = ph;
+    m[i] = pm;
+    l[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2));
+  }
+  Split3 s;
+  s.hi = __builtin_bit_cast(bf16x8, h);
+  s.mid = __builtin_bit_cast(bf16x8, m);
+  s.lo = __builtin_bit_cast(bf16x8, l);
+  return s;
+}
+
+// The weight planes of one 16-deep K step for the wave's NR column tiles
+// (plane p of step g of column tile nt: block (nt * G16 + g) * 3 + p of 64 lanes x 16 B).
+template <int NR>
+struct WStep {
+  bf16x8 p[NR][3];
+};
+
+template <int NR>
+__device__ __forceinline__ void load_w(WStep<NR> &w, const bf16x8 *const (&bp)[NR], int g) {
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int p = 0; p < 3; ++p) w.p[j][p] = bp[j][((size_t)g * 3 + p) * 64];
+}
+
+// A fragments of K step g (lane: row lane&31, k 16g + 8*(lane>>5) + 0..7), two ds_read_b128.
+template <int MR>
+__device__ __forceinline__ void load_a(f32x8 (&a)[MR], const float *ap, int g) {
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const f32x4 *q = reinterpret_cast<const f32x4 *>(ap + m * 32 * kLd + 16 * g);
+    const f32x4 lo4 = q[0], hi4 = q[1];
+    a[m] = f32x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+  }
+}
+
+// One K step: the 6 * MR * NR MFMAs of step g (A already split, in sa) with the
+// operand traffic of later steps in their shadow -- the weight planes of step
+// g+2 (into the buffer step g-1 used: three buffers in flight, two steps of
+// L2 latency covered) and A of step g+1, read from LDS and split in VALU
+// between the MFMAs (sched_group_barrier pattern below), into sa for the next step.
+template <int MR, int NR>
+__device__ __forceinline__ void step_x(Split3 (&sa)[MR], const WStep<NR> &w, WStep<NR> &fill,
+                                       const bf16x8 *const (&bp)[NR], const float *ap, int g,
+                                       int last, f32x16 (&acc)[MR][NR]) {
+  __builtin_amdgcn_sched_barrier(0);
+  load_w(fill, bp, min(g + 2, last));
+  f32x8 an[MR];
+  load_a(an, ap, min(g + 1, last));
+  Split3 sn[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) sn[m] = split3(an[m]);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      f32x16 c = acc[m][j];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].lo, w.p[j][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].mid, w.p[j][1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].hi, w.p[j][2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].mid, w.p[j][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].hi, w.p[j][1], c, 0, 0, 0);
+      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].hi, w.p[j][0], c, 0, 0, 0);
+    }
+  // issue order: the loads, a few MFMAs to cover the LDS latency, then the
+  // split VALU two instructions per MFMA gap
+  constexpr int kMfma = 6 * MR * NR, kLead = (kMfma >= 12) ? 6 : kMfma / 2;
+  __builtin_amdgcn_sched_group_barrier(0x020, 3 * NR, 0);  // VMEM reads
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * MR, 0);  // DS reads
+  __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
+#pragma unroll
+  for (int i = 0; i < kMfma - kLead; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int m = 0; m < MR; ++m) sa[m] = sn[m];
+}
+
+// Full-width layer in bf16x6 mode (NR column tiles per wave).
+template <int MR, int NR>
+__device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__restrict__ wx,
+                                             int G16, int wave, int lane, f32x16 (&acc)[MR][NR]) {
+  const int r = lane & 31, h = lane >> 5;
+  const float *ap = H + r * kLd + 8 * h;
+  const bf16x8 *bp[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    bp[j] = wx + (size_t)(wave + kWaves * j) * G16 * 3 * 64 + lane;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
+  }
+  const int last = G16 - 1;
+  WStep<NR> w0, w1, w2;
+  load_w(w0, bp, 0);
+  load_w(w1, bp, min(1, last));
+  Split3 sa[MR];
+  {
+    f32x8 a0[MR];
+    load_a(a0, ap, 0);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) sa[m] = split3(a0[m]);
+  }
+  int g = 0;
+  for (; g + 3 <= G16; g += 3) {
+    step_x<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
+    step_x<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
+    step_x<MR, NR>(sa, w2, w1, bp, ap, g + 2, last, acc);
+  }
+  if (g < G16) step_x<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
+  if (g + 1 < G16) step_x<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
+}
+
+// One Dense layer for a wave with NR column tiles.  wx: the layer's split-bf16
+// weight planes (bf16x6 mode, full-width layers only), else nullptr.
 template <int MR, int NR>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
-                                          int G, int wave, int lane, unsigned long long *st) {
+                                          int G, int wave, int lane, unsigned long long *st,
+                                          const bf16x8 *wx = nullptr, int G16 = 0) {
   f32x16 acc[MR][NR];
-  layer_gemm<MR, NR>(H, wp, G, 0, G, wave, kWaves, lane, acc);
+  if (wx)
+    layer_gemm_x<MR, NR>(H, wx, G16, wave, lane, acc);
+  else
+    layer_gemm<MR, NR>(H, wp, G, 0, G, wave, kWaves, lane, acc);
   switch (act) {
     case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bias, wave, lane, acc, st); break;
     case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bias, wave, lane, acc, st); break;
@@ -283,7 +436,9 @@ __device__ __forceinline__ double fk_error(const double *jc, const double th[4],
   return ok ? dist3(e, p) : __builtin_nan("");
 }
 
-template <int MR>
+// X: bf16x6 mode -- layers whose split weight planes exist (a.m.wx[l]) take
+// the split-bf16 GEMM; the others (input layer, split-K output layer) stay fp32.
+template <int MR, bool X>
 __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnArgs a) {
   constexpr int BM = 32 * MR;
   __shared__ __attribute__((aligned(16))) float H[BM * kLd];
@@ -329,8 +484,19 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
       const float *bias = a.m.bias[l];
       const int act = a.m.act[l];
       unsigned long long *sl = (stp && l < 14) ? stp + 2 + 2 * l : nullptr;
+      const bf16x8 *wx = X ? reinterpret_cast<const bf16x8 *>(a.m.wx[l]) : nullptr;
       if (NT == 1) {
         run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid, sl);
+      } else if (X && wx) {
+        const int G16 = (a.m.kp[l] + 15) >> 4;
+        const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
+        switch (cnt) {
+          case 4: run_layer<MR, 4>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
+          case 3: run_layer<MR, 3>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
+          case 2: run_layer<MR, 2>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
+          case 1: run_layer<MR, 1>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
+          default: __syncthreads(); break;
+        }
       } else {
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
@@ -385,6 +551,14 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
   }
 }
 
+// The bf16x6 kernels are instantiated in a translation unit of their own
+// (ik_ann_x.hip defines IKHIP_ANN_X_TU and includes this file): in one module
+// with the fp32 kernel they change the latter's register allocation (29 -> 51
+// spilled VGPRs at MR = 2, -Rpass-analysis=kernel-resource-usage).
+void launch_ann_kernel_x(int mr, unsigned grid, hipStream_t st, const AnnArgs &a);
+
+#ifndef IKHIP_ANN_X_TU
+
 size_t ann_packed_floats(int k, int n) {
   int kp = (k + 7) / 8 * 8, np = (n + 31) / 32 * 32;
   return (size_t)kp * np;
@@ -405,6 +579,55 @@ void ann_pack_layer(const float *W, int k, int n, float *dst) {
           int c = nt * 32 + (lane & 31);
           dst[(((size_t)nt * G + g) * 64 + lane) * 4 + s] =
               (kk < k && c < n) ? W[(size_t)kk * n + c] : 0.0f;
+        }
+}
+
+size_t ann_x_bytes(int k, int n) {
+  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
+  return (size_t)k16 * np * 6;
+}
+
+static uint16_t bf16_rne(float x) {
+  uint32_t u;
+  std::memcpy(&u, &x, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);  // inf / nan (none expected)
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+static float bf16_to_f32(uint16_t h) {
+  uint32_t u = (uint32_t)h << 16;
+  float x;
+  std::memcpy(&x, &u, 4);
+  return x;
+}
+
+// The bf16x6 weight operand: three bf16 planes p (0 hi, 1 mid, 2 lo) of the B
+// fragment of v_mfma_f32_32x32x16_bf16 for K step g of column tile nt, element
+// j (0..7) of lane l being W[16g + 8*(l>>5) + j][32nt + (l&31)]:
+// dst[(((nt*G16 + g)*3 + p)*64 + l)*8 + j], split here by round-to-nearest-even
+// exactly as split3() splits the activations on the GPU.  (An fp32 layout split
+// in the kernel reads 4 B per weight instead of 6 but measured slower at
+// 64-point tiles: 30.5 vs 27.3 ms per 1M points, the VALU being the dearer.)
+void ann_pack_layer_x(const float *W, int k, int n, void *dst) {
+  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
+  int G16 = k16 / 16, NT = np / 32;
+  uint16_t *d16 = static_cast<uint16_t *>(dst);
+  for (int nt = 0; nt < NT; ++nt)
+    for (int g = 0; g < G16; ++g)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int kk = 16 * g + 8 * (lane >> 5) + j;
+          const int c = nt * 32 + (lane & 31);
+          const float x = (kk < k && c < n) ? W[(size_t)kk * n + c] : 0.0f;
+          const uint16_t h = bf16_rne(x);
+          const float r1 = x - bf16_to_f32(h);
+          const uint16_t m = bf16_rne(r1);
+          const float r2 = r1 - bf16_to_f32(m);
+          const size_t base = (((size_t)nt * G16 + g) * 3) * 64 * 8 + (size_t)lane * 8 + j;
+          d16[base] = h;
+          d16[base + 64 * 8] = m;
+          d16[base + 2 * 64 * 8] = bf16_rne(r2);
         }
 }
 
@@ -455,12 +678,27 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   const int64_t ntiles = (n + bm - 1) / bm;
   const int64_t slots = (int64_t)cus * (mr == 2 ? 1 : 2);  // resident workgroups
   unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);
-  kt_begin("ann_fused_kernel", st);
-  if (mr == 2)
-    hipLaunchKernelGGL(ann_fused_kernel<2>, dim3(grid), dim3(256), 0, st, a);
+  bool x = false;
+  for (int l = 0; l < m.n_layers; ++l) x = x || m.wx[l] != nullptr;
+  kt_begin(x ? "ann_fused_kernel_bf16x6" : "ann_fused_kernel", st);
+  if (x)
+    launch_ann_kernel_x(mr, grid, st, a);
+  else if (mr == 2)
+    hipLaunchKernelGGL((ann_fused_kernel<2, false>), dim3(grid), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL(ann_fused_kernel<1>, dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ann_fused_kernel<1, false>), dim3(grid), dim3(256), 0, st, a);
   kt_end(st);
 }
+
+#else  // IKHIP_ANN_X_TU
+
+void launch_ann_kernel_x(int mr, unsigned grid, hipStream_t st, const AnnArgs &a) {
+  if (mr == 2)
+    hipLaunchKernelGGL((ann_fused_kernel<2, true>), dim3(grid), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((ann_fused_kernel<1, true>), dim3(grid), dim3(256), 0, st, a);
+}
+
+#endif  // IKHIP_ANN_X_TU
 
 }  // namespace ikhip

@@ -76,6 +76,8 @@ struct ik_ctx {
   bool ann_loaded = false;
   AnnModelDev ann;
   void *ann_buf = nullptr;
+  const void *ann_wx[kAnnMaxLayers] = {};  // bf16x6 weight operand of each layer (or null)
+  int ann_mode = IK_ANN_FP32;
   int fabrik_variant = 1;
   KTimer kt;
   unsigned long long *dbg = nullptr;  // diagnostic stamp buffer (ik_ctx_set_debug)
@@ -193,6 +195,8 @@ int ik_ctx_create(int device, ik_ctx **out) {
   std::memcpy(c->robot.links, kDefaultLinks, sizeof(kDefaultLinks));
   std::memcpy(c->robot.lim, kDefaultLimits, sizeof(kDefaultLimits));
   if (const char *v = std::getenv("IKHIP_FABRIK_VARIANT")) c->fabrik_variant = std::atoi(v);
+  if (const char *v = std::getenv("IKHIP_ANN_MODE"))
+    if (std::strcmp(v, "bf16x6") == 0) c->ann_mode = IK_ANN_BF16X6;
   *out = c;
   return IK_OK;
 }
@@ -465,8 +469,11 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
       return fail(IK_E_BADARG, "ik_ann_load: unsupported activation code");
   int rc = set_dev(c);
   if (rc) return rc;
-  // one device buffer: per layer packed weights then padded bias
-  std::vector<size_t> woff(n_layers), boff(n_layers);
+  // one device buffer: per layer packed weights, padded bias and -- for the
+  // hidden layers that can take the bf16x6 mode (not the input layer, not a
+  // single-column-tile output layer) -- the split bf16 planes
+  std::vector<size_t> woff(n_layers), boff(n_layers), xoff(n_layers, 0);
+  auto splittable = [&](int l) { return l > 0 && (dims[l + 1] + 31) / 32 > 1; };
   size_t total = 0;
   for (int l = 0; l < n_layers; ++l) {
     woff[l] = total;
@@ -475,11 +482,18 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
     boff[l] = total;
     total += (size_t)((dims[l + 1] + 31) / 32 * 32) * 4;
     total = (total + 255) & ~(size_t)255;
+    if (splittable(l)) {
+      xoff[l] = total;
+      total += ann_x_bytes(dims[l], dims[l + 1]);
+      total = (total + 255) & ~(size_t)255;
+    }
   }
   std::vector<char> host(total, 0);
   for (int l = 0; l < n_layers; ++l) {
     ann_pack_layer(W[l], dims[l], dims[l + 1], reinterpret_cast<float *>(&host[woff[l]]));
     std::memcpy(&host[boff[l]], b[l], (size_t)dims[l + 1] * 4);
+    if (splittable(l))
+      ann_pack_layer_x(W[l], dims[l], dims[l + 1], &host[xoff[l]]);
   }
   IK_HIP(hipStreamSynchronize(c->stream));
   if (c->ann_buf) IK_HIP(hipFree(c->ann_buf));
@@ -497,6 +511,7 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
     m.act[l] = acts[l];
     m.wp[l] = reinterpret_cast<const float4 *>(base + woff[l]);
     m.bias[l] = reinterpret_cast<const float *>(base + boff[l]);
+    c->ann_wx[l] = splittable(l) ? base + xoff[l] : nullptr;
   }
   for (int i = 0; i < 3; ++i) {
     m.xm[i] = x_mean[i];
@@ -509,6 +524,16 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   c->ann_loaded = true;
   return IK_OK;
 }
+
+int ik_ann_set_mode(ik_ctx *c, int mode) {
+  if (!c) return fail(IK_E_BADARG, "ik_ann_set_mode: NULL context");
+  if (mode != IK_ANN_FP32 && mode != IK_ANN_BF16X6)
+    return fail(IK_E_BADARG, "ik_ann_set_mode: unknown mode");
+  c->ann_mode = mode;
+  return IK_OK;
+}
+
+int ik_ann_get_mode(ik_ctx *c) { return c ? c->ann_mode : -IK_E_BADARG; }
 
 int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk_err,
                  int flags, ik_stats *stats) {
@@ -534,7 +559,10 @@ int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk
     de = fk_err ? reinterpret_cast<double *>(s + b_in + b_a) : nullptr;
   }
   launch_reset_stats(c->d_stats, c->stream);
-  launch_ann(c->ann, c->robot, dp, n, da, de, !(flags & IK_F_NO_LIMITS), c->d_stats, c->stream,
+  AnnModelDev m = c->ann;
+  for (int l = 0; l < m.n_layers; ++l)
+    m.wx[l] = (c->ann_mode == IK_ANN_BF16X6) ? c->ann_wx[l] : nullptr;
+  launch_ann(m, c->robot, dp, n, da, de, !(flags & IK_F_NO_LIMITS), c->d_stats, c->stream,
              c->dbg);
   IK_HIP(hipGetLastError());
   if (!dev && n > 0) {

@@ -1,6 +1,7 @@
 """Time the fused ANN kernel (reference architecture, 1M points) under each
-tile variant (IKHIP_ANN_MR=1|2), in fresh subprocesses; checks the result
-against a float64 numpy forward on the first 2048 points."""
+tile variant (IKHIP_ANN_MR=1|2) and GEMM mode (IKHIP_ANN_MODE=fp32|bf16x6), in
+fresh subprocesses; checks the result against a float64 numpy forward on the
+first 2048 points."""
 import json
 import os
 import subprocess
@@ -29,7 +30,8 @@ ts = []
 for _ in range(5):
     ctx.ann_solve_device(pts, ang, err, flags=F)
     ts.append(sum(v for k, v in ctx.kernel_times()))
-ref = O.ann_forward(p[:2048], m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+ref = O.ann_forward(p[:2048], m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale,
+                    compute=np.float64)
 d = float(np.abs(ang[:2048].cpu().numpy().astype(np.float64) - ref).max())
 print(json.dumps({"ms": min(ts), "ms_med": sorted(ts)[2], "max_abs_diff": d,
                   "tflops": 5.507e6 * n / (min(ts) / 1e3) / 1e12}))
@@ -37,10 +39,12 @@ print(json.dumps({"ms": min(ts), "ms_med": sorted(ts)[2], "max_abs_diff": d,
 
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-    for mr in ("1", "2"):
-        e = dict(os.environ, IKHIP_ANN_MR=mr)
+    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fp32", "bf16x6"]
+    for mode in modes:
+      for mr in ("1", "2"):
+        e = dict(os.environ, IKHIP_ANN_MR=mr, IKHIP_ANN_MODE=mode)
         out = subprocess.run([sys.executable, "-c", CODE, str(n)], env=e, capture_output=True,
                              text=True, timeout=600)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
-        print(json.dumps({"MR": mr, **(json.loads(line[-1]) if line else
+        print(json.dumps({"MR": mr, "mode": mode, **(json.loads(line[-1]) if line else
                                        {"error": out.stderr[-800:]})}), flush=True)
