@@ -30,6 +30,8 @@ sys.path.insert(0, ROOT)
 METRIC = "IK solutions/sec (6DOF, 1M-point batch) at 1/2/4/8 GPUs; max |FK err|"
 ANN_DIMS = (3,) + (500,) * 12 + (4,)
 FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: dense fp32 matrix peak
+BF16_MFMA_PEAK = 2.5e15     # dense bf16 matrix peak (no sparsity)
+BF16X6_PRODUCTS = 6         # bf16 MFMA products per fp32 product in the bf16x6 mode
 FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
 HBM_PEAK = 8.0e12           # bytes/s
 FABRIK_FLOP_PER_ITER = 132
@@ -48,6 +50,9 @@ def parse():
                     help="CPU-baseline time budget (rank 0, N=1); 0 disables")
     ap.add_argument("--secondary", type=int, default=1,
                     help="also time the other method and report it under 'secondary'")
+    ap.add_argument("--ann-mode", choices=["fp32", "bf16x6"], default="fp32",
+                    help="ANN hidden-GEMM arithmetic of the headline line (ikhip.h "
+                         "ik_ann_set_mode); the other mode is reported under 'secondary'")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--gather", type=int, default=0,
                     help="N>1: include the RCCL all_gather of every rank's angle rows in the "
@@ -123,13 +128,14 @@ def make_gather(dang, args, world):
     return gather
 
 
-def run_ann(ctx, dpts, n, args, world):
+def run_ann(ctx, dpts, n, args, world, mode="fp32"):
     import torch
     from inversekinematicsann_amd import _native
     from inversekinematicsann_amd.kinematics.ann import (REFERENCE_X_SCALER as XS,
                                                          REFERENCE_Y_SCALER as YS, glorot_model)
     m = glorot_model(ANN_DIMS, seed=0)
     ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    ctx.ann_set_mode(mode)
     dang = torch.empty((n, 4), dtype=torch.float32, device="cuda")
     derr = torch.empty(n, dtype=torch.float64, device="cuda")
     flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
@@ -144,19 +150,30 @@ def run_ann(ctx, dpts, n, args, world):
     st = ctx.stats_fetch()
     res["max_fk_err"] = max_over_ranks(st.max_fk_err, world)
     res["mean_fk_err"] = sum_over_ranks(st.sum_fk_err, world) / (n * world)
+    ctx.ann_set_mode("fp32")
     flop_pt = m.flops_per_point()
-    k = res["kernels"].get("ann_fused_kernel")
+    kname = "ann_fused_kernel" if mode == "fp32" else "ann_fused_kernel_bf16x6"
+    k = res["kernels"].get(kname)
     achieved = flop_pt * n / (k / 1e3) if k else None
-    traffic = load_traffic(args.traffic_file, "ann_fused_kernel")
+    # bf16x6: six bf16 MFMA products per fp32 product, so the fp32-equivalent
+    # matrix peak is the bf16 peak / 6 (the input and output layers stay fp32)
+    peak = FP32_MFMA_PEAK if mode == "fp32" else BF16_MFMA_PEAK / BF16X6_PRODUCTS
+    traffic = load_traffic(args.traffic_file, kname)
     res["roofline"] = {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
-                       "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-                       "frac": achieved / FP32_MFMA_PEAK if achieved else None,
-                       "traffic": traffic, "kernel": "ann_fused_kernel",
+                       "peak": peak / 1e12, "unit": "TFLOP/s",
+                       "frac": achieved / peak if achieved else None,
+                       "traffic": traffic, "kernel": kname,
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
                        "points_per_launch": n}
-    res["dtype"] = "fp32"
-    res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
-                       "1M random_dist points per GPU")
+    if mode == "fp32":
+        res["dtype"] = "fp32"
+        res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
+                           "1M random_dist points per GPU")
+    else:
+        res["dtype"] = "fp32 via bf16x6 (3-way bf16 split, 6 MFMA products, fp32 accumulate)"
+        res["workload"] = ("ANN MLP forward (3-12x500tanh-4), hidden GEMMs in the bf16x6 mode "
+                           "(fp32-accurate: tests/test_gpu_parity.py::test_ann_bf16x6_mode) + "
+                           "fused FK round-trip error, 1M random_dist points per GPU")
     return res
 
 
@@ -284,17 +301,20 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    runners = {"ann": run_ann, "fabrik": run_fabrik}
+    other_mode = "bf16x6" if args.ann_mode == "fp32" else "fp32"
+    runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik,
+               f"ann_{other_mode}": lambda *a: run_ann(*a, mode=other_mode)}
     res = runners[args.method](ctx, dpts, n, args, world)
     secondary = {}
     if args.secondary:
-        other = "fabrik" if args.method == "ann" else "ann"
-        r2 = runners[other](ctx, dpts, n, args, world)
-        secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
-                            "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
-                            "roofline": r2["roofline"], "workload": r2["workload"],
-                            **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "mean_iters",
-                                                  "n_capped") if k in r2}}
+        others = ["fabrik", f"ann_{other_mode}"] if args.method == "ann" else ["ann"]
+        for other in others:
+            r2 = runners[other](ctx, dpts, n, args, world)
+            secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
+                                "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
+                                "roofline": r2["roofline"], "workload": r2["workload"],
+                                **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "mean_iters",
+                                                      "n_capped") if k in r2}}
     total = n * world
     value = total / (res["ms_per_step"] / 1e3)
     line = {
@@ -307,6 +327,7 @@ def main():
                 "(the reference .h5 is not shipped); reference StandardScaler constants",
         "config": {"workload": res["workload"], "points_per_gpu": n, "total_points": total,
                    "parallelism": f"dp{world}", "method": args.method,
+                   "ann_mode": args.ann_mode if args.method == "ann" else None,
                    "all_gather_in_step": bool(args.gather and world > 1),
                    "tol": args.tol if args.method == "fabrik" else None,
                    "max_iter": args.max_iter if args.method == "fabrik" else None},
@@ -324,6 +345,8 @@ def main():
         if args.secondary:
             other = "fabrik" if args.method == "ann" else "ann"
             line["secondary"][other]["cpu_baseline"] = cpu_baseline(other, args)
+            if other_mode == "bf16x6" and f"ann_{other_mode}" in line["secondary"]:
+                line["secondary"]["ann_bf16x6"]["cpu_baseline"] = "see top-level cpu_baseline"
     if rank == 0:
         print(json.dumps(line), flush=True)
     if _dist_on():

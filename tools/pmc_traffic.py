@@ -26,6 +26,8 @@ KERNELS = ("ann_fused_kernel", "fabrik_iter_kernel", "fabrik_seed_kernel",
 
 
 def _short(name: str) -> str | None:
+    if "ann_fused_kernel" in name and "true" in name:  # ann_fused_kernel<MR, true>: bf16x6 mode
+        return "ann_fused_kernel_bf16x6"
     for k in KERNELS:
         if k in name:
             return k
