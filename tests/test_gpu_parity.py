@@ -203,6 +203,9 @@ def _ann_case(ctx, dims, acts_hidden, n, seed, check_limits=False, fk=False):
     ((3, 512, 512, 4), "relu"),
     ((3, 96, 96, 4), "sigmoid"),
     ((3, 4), "linear"),
+    # full-width layers whose K is padded to 64 past what the layer before wrote
+    ((3, 450, 500, 4), "tanh"),
+    ((3, 70, 512, 4), "sigmoid"),
 ])
 def test_ann_vs_oracle(ctx1, dims, act):
     n = 4099  # not a multiple of the 64-point tile
