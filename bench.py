@@ -150,6 +150,10 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
     st = ctx.stats_fetch()
     res["max_fk_err"] = max_over_ranks(st.max_fk_err, world)
     res["mean_fk_err"] = sum_over_ranks(st.sum_fk_err, world) / (n * world)
+    res["p99_fk_err"] = max_over_ranks(float(torch.quantile(derr[:1 << 24], 0.99)), world)
+    res["outputs"] = {"ang": dang}
+    res["end_to_end"] = end_to_end(
+        lambda hp: ctx.ann_solve(hp, check_limits=True, want_fk_err=True), dpts, args, world)
     ctx.ann_set_mode("fp32")
     flop_pt = m.flops_per_point()
     kname = "ann_fused_kernel" if mode == "fp32" else "ann_fused_kernel_bf16x6"
@@ -194,6 +198,9 @@ def run_fabrik(ctx, dpts, n, args, world):
     st = ctx.stats_fetch()
     res["mean_iters"] = st.sum_iters / n
     res["n_capped"] = st.n_capped
+    res["outputs"] = {"ang": dang, "iters": dit}
+    res["end_to_end"] = end_to_end(
+        lambda hp: ctx.fabrik_solve(hp, args.tol, args.max_iter), dpts, args, world)
     k = res["kernels"].get("fabrik_iter_kernel")
     flops = FABRIK_FLOP_PER_ITER * st.sum_iters
     achieved = flops / (k / 1e3) if k else None
@@ -242,8 +249,30 @@ def timed(ctx, step, args, world):
             "kernels": kernels}
 
 
-def cpu_baseline(method, args):
-    """The oracle timed on this host (rank 0, N=1) over a bounded sample."""
+def end_to_end(solve_host, dpts, args, world):
+    """PCIe-inclusive rate (SURVEY 8(d) "end-to-end"): host float64 points in,
+    host angles out through the library's host-pointer path (H2D, kernels,
+    D2H, stats), pageable numpy buffers.  Reported beside `value`, never as it."""
+    import torch
+    pts = dpts.cpu().numpy()
+    reps = max(1, min(args.steps, 3))
+    solve_host(pts)  # warm the staging scratch
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        solve_host(pts)
+    torch.cuda.synchronize()
+    barrier(world)
+    wall = max_over_ranks(time.perf_counter() - t0, world)
+    ms = wall * 1e3 / reps
+    return {"ms_per_step": ms, "value": pts.shape[0] * world / (ms / 1e3), "steps": reps,
+            "unit": "IK solutions/s", "path": "host pointers (ik_*_solve without IK_F_DEVICE)"}
+
+
+def cpu_baseline(method, args, sample_pts=None, gpu_out=None):
+    """The oracle timed on this host (rank 0, N=1) over a bounded sample, which
+    is the first points of the GPU batch: the oracle's results on it are also
+    the bench's parity check of the GPU output."""
     from oracle import oracle as O
     from inversekinematicsann_amd.robot.position_generator import random_dist
     budget = args.cpu_seconds
@@ -259,30 +288,46 @@ def cpu_baseline(method, args):
                                                              glorot_model)
         m = glorot_model(ANN_DIMS, seed=0)
         chunk = 8192
-        pts = random_dist(chunk, seed=99)
-        done, t0 = 0, time.perf_counter()
+        pts = sample_pts[:chunk] if sample_pts is not None else random_dist(chunk, seed=99)
+        done, t0, first = 0, time.perf_counter(), None
         while True:
-            O.ann_forward(pts, m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean,
-                          YS.scale, compute=np.float32)
+            out = O.ann_forward(pts, m.weights, m.biases, m.activations, XS.mean, XS.scale,
+                                YS.mean, YS.scale, compute=np.float32)
+            first = out if first is None else first
             done += chunk
             if time.perf_counter() - t0 >= budget:
                 break
         el = time.perf_counter() - t0
-        return {"value": done / el, "unit": "IK solutions/s", "cores": threads, "kind": "port",
-                "sample": f"{done} random_dist points in {chunk}-point batches, numpy fp32 MLP "
-                          f"(oracle.ann_forward) on {threads} BLAS threads, {el:.1f} s"}
+        res = {"value": done / el, "unit": "IK solutions/s", "cores": threads, "kind": "port",
+               "sample": f"{done} points (the GPU batch's first {chunk}, repeated) in "
+                         f"{chunk}-point batches, numpy fp32 MLP (oracle.ann_forward) on "
+                         f"{threads} BLAS threads, {el:.1f} s"}
+        if gpu_out is not None:
+            d = float(np.abs(gpu_out["ang"][:chunk].astype(np.float64) - first).max())
+            res["parity"] = {"points": chunk, "max_abs_diff_vs_oracle_fp32": d,
+                             "tolerance": 1e-5, "ok": d <= 1e-5}
+        return res
     chunk = 4096
-    pts = random_dist(chunk, seed=99)
-    done, t0 = 0, time.perf_counter()
+    pts = sample_pts[:chunk] if sample_pts is not None else random_dist(chunk, seed=99)
+    done, t0, first = 0, time.perf_counter(), None
     while True:
-        O.fabrik_ikine(pts, args.tol, args.max_iter)
+        out = O.fabrik_ikine(pts, args.tol, args.max_iter)
+        first = out if first is None else first
         done += chunk
         if time.perf_counter() - t0 >= budget:
             break
     el = time.perf_counter() - t0
-    return {"value": done / el, "unit": "IK solutions/s", "cores": 1, "kind": "port",
-            "sample": f"{done} random_dist points, C oracle (oracle/ik_oracle.c, scalar, "
-                      f"1 thread), tol {args.tol:g}/{args.max_iter}, {el:.1f} s"}
+    res = {"value": done / el, "unit": "IK solutions/s", "cores": 1, "kind": "port",
+           "sample": f"{done} points (the GPU batch's first {chunk}, repeated), C oracle "
+                     f"(oracle/ik_oracle.c, scalar, 1 thread), tol {args.tol:g}/{args.max_iter}, "
+                     f"{el:.1f} s"}
+    if gpu_out is not None:
+        ang_ref, it_ref = first[0], first[1]
+        d = float(np.abs(gpu_out["ang"][:chunk] - ang_ref).max())
+        same = int((gpu_out["iters"][:chunk] == it_ref).sum())
+        res["parity"] = {"points": chunk, "max_abs_diff": d, "tolerance": 1e-5,
+                         "iters_equal": same, "ok": d <= 1e-5 and same == chunk}
+    return res
 
 
 def main():
@@ -305,6 +350,7 @@ def main():
     runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik,
                f"ann_{other_mode}": lambda *a: run_ann(*a, mode=other_mode)}
     res = runners[args.method](ctx, dpts, n, args, world)
+    outputs = {args.method: res["outputs"]}
     secondary = {}
     if args.secondary:
         others = ["fabrik", f"ann_{other_mode}"] if args.method == "ann" else ["ann"]
@@ -313,8 +359,10 @@ def main():
             secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
                                 "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
                                 "roofline": r2["roofline"], "workload": r2["workload"],
-                                **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "mean_iters",
-                                                      "n_capped") if k in r2}}
+                                **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
+                                                      "mean_iters", "n_capped", "end_to_end")
+                                   if k in r2}}
+            outputs[other] = r2["outputs"]
     total = n * world
     value = total / (res["ms_per_step"] / 1e3)
     line = {
@@ -335,16 +383,19 @@ def main():
         "event_ms_per_step": res["event_ms_per_step"],
         "kernels_ms": res["kernels"],
     }
-    for k in ("max_fk_err", "mean_fk_err", "mean_iters", "n_capped"):
+    for k in ("max_fk_err", "mean_fk_err", "p99_fk_err", "mean_iters", "n_capped", "end_to_end"):
         if k in res:
             line[k] = res[k]
     if secondary:
         line["secondary"] = secondary
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(args.method, args)
+        def host(o):
+            return {k: v[:8192].cpu().numpy() for k, v in o.items()}
+        line["cpu_baseline"] = cpu_baseline(args.method, args, pts, host(outputs[args.method]))
         if args.secondary:
             other = "fabrik" if args.method == "ann" else "ann"
-            line["secondary"][other]["cpu_baseline"] = cpu_baseline(other, args)
+            line["secondary"][other]["cpu_baseline"] = cpu_baseline(other, args, pts,
+                                                                    host(outputs[other]))
             if other_mode == "bf16x6" and f"ann_{other_mode}" in line["secondary"]:
                 line["secondary"]["ann_bf16x6"]["cpu_baseline"] = "see top-level cpu_baseline"
     if rank == 0:
