@@ -97,3 +97,21 @@ def test_cli_ann_keras_h5_model(tmp_path, capsys):
     ref = O.ann_forward(pd.read_csv(pts_csv).values, m.weights, m.biases, m.activations,
                         xs.mean, xs.scale, ys.mean, ys.scale)
     assert np.abs(pd.read_csv(out).values - ref).max() <= 1e-5
+
+
+def test_rpc_handler_on_gpu_engine():
+    """rpc_broker.py contract on the GPU FABRIK engine: spring(20) angles match
+    the reference-recorded goldens, an out-of-reach request answers ERROR with
+    the reference's message for a Point (inverse.py:32)."""
+    from inversekinematicsann_amd.rpc_broker import IkineRequestHandler, get_ikine_engine_cli
+    g = np.load(os.path.join(GOLDEN, "fabrik_spring20.npz"), allow_pickle=False)
+    h = IkineRequestHandler(get_ikine_engine_cli(["--method", "fabrik"]))
+    out = json.loads(h.handle(json.dumps({"positions": g["points"].tolist()}).encode(), "id7"))
+    assert out["status"] == "OK" and list(out) == ["status", "angles"]
+    assert np.abs(np.array(out["angles"]) - g["angles"]).max() <= 1e-9  # north_star: 1e-5
+    bad = {"positions": [[1.0, 2.1, 3.0], [1.567, 2.22, -3.123]]}
+    out = json.loads(h.handle(json.dumps(bad).encode(), "id8"))
+    assert out == {"status": "ERROR", "correlation_id": "id8",
+                   "reason": "Inverse Kinematics exception, point Point(1.567, 2.22, -3.123) is "
+                             "out of manipulator reach area! Limits: {'x': [0, 6], "
+                             "'y': [-6, 6], 'z': [-3, 6]}"}
