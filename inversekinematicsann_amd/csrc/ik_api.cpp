@@ -81,6 +81,7 @@ struct ik_ctx {
   int fabrik_variant = 1;
   KTimer kt;
   unsigned long long *dbg = nullptr;  // diagnostic stamp buffer (ik_ctx_set_debug)
+  FabOrderDev *fab_ord = nullptr;     // FABRIK work-order cost table (learned per robot)
 };
 
 namespace {
@@ -186,6 +187,8 @@ int ik_ctx_create(int device, ik_ctx **out) {
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc(&c->d_stats, sizeof(DevStats));
   if (e == hipSuccess) e = hipHostMalloc(&c->h_stats, sizeof(DevStats), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMalloc(&c->fab_ord, sizeof(FabOrderDev));
+  if (e == hipSuccess) e = hipMemset(c->fab_ord, 0, sizeof(FabOrderDev));
   if (e != hipSuccess) {
     delete c;
     return fail(IK_E_HIP, std::string("ik_ctx_create: ") + hipGetErrorString(e));
@@ -209,6 +212,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->ann_buf) (void)hipFree(c->ann_buf);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->dbg) (void)hipFree(c->dbg);
+  if (c->fab_ord) (void)hipFree(c->fab_ord);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   for (int i = 0; i < kMaxTimed; ++i) {
@@ -229,9 +233,17 @@ void *ik_ctx_get_stream(ik_ctx *c) { return c ? static_cast<void *>(c->stream) :
 
 int ik_set_robot(ik_ctx *c, const double *dh, const double *links, const double *limits) {
   if (!c) return fail(IK_E_BADARG, "ik_set_robot: NULL context");
+  const RobotDev old = c->robot;
   if (dh) std::memcpy(c->robot.dh, dh, sizeof(c->robot.dh));
   if (links) std::memcpy(c->robot.links, links, sizeof(c->robot.links));
   if (limits) std::memcpy(c->robot.lim, limits, sizeof(c->robot.lim));
+  // the FABRIK cost table describes one chain: forget it when the chain changes
+  if (std::memcmp(old.dh, c->robot.dh, sizeof(old.dh)) ||
+      std::memcmp(old.links, c->robot.links, sizeof(old.links))) {
+    int rc = set_dev(c);
+    if (rc) return rc;
+    IK_HIP(hipMemsetAsync(c->fab_ord, 0, sizeof(FabOrderDev), c->stream));
+  }
   return IK_OK;
 }
 
@@ -387,7 +399,7 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
   launch_reset_stats(c->d_stats, c->stream);
   launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj,
                       !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
-                      c->fabrik_variant);
+                      c->fabrik_variant, c->fab_ord);
   IK_HIP(hipGetLastError());
   if (!dev && n > 0) {
     IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));

@@ -100,6 +100,15 @@ struct FabArgs {
   uint8_t *status; // split pipeline scratch (n)
   DevStats *S;
   int chunk;       // work-queue grab size of the persistent iteration kernel
+  // hard-first ordering (see "Work order" below); unused when perm is null
+  int32_t *perm;            // queue position -> point index
+  int32_t *iperm;           // point index -> queue position
+  uint8_t *status_in;       // ordered: the seed status by point (status is by position)
+  uint16_t *cell;           // per point: goal cell (bits 0-9) | cost class << 10
+  FabOrderDev *ord;         // context-owned cost table and class histogram
+  int nseg, seg_blocks;     // histogram segments, and blocks per segment
+  int32_t *iters_out;       // ordered: the caller's iterations (by point), nullable
+  double *joints_out;       // ordered: the caller's final joints (by point), nullable
 };
 
 static int env_int(const char *name, int dflt) {
@@ -139,24 +148,199 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
 }
 
 // -------------------------------------------------------------- split ----
-// 1. limits + seed pose (uniform work, one point per lane)
+// 1. limits + seed pose (uniform work, one point per lane).  ORD (work order
+// below): also the goal's cell and the per-segment counts of its cost class.
+template <bool ORD>
+__global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a);
+
+// ---------------------------------------------------------- Work order ----
+// The persistent iteration kernel hands points out in queue order.  In point
+// order a 100-iteration point can be picked up just before the queue runs dry
+// and set the launch length alone (≈ 1.4x the lane-iterations / lanes bound
+// at 1M random_dist points).  Handing out the expensive points first removes
+// most of that tail (a list-scheduling simulation of the kernel's refill rule
+// on reference iteration counts: 1.44x -> 1.09x the bound).  The cost of a
+// point is predicted from its goal cell -- distance from the shoulder (the
+// first joint) in 64 bins up to the reach of links 1..3, and the sine of the
+// elevation in 16 bins -- by the mean iteration count the context recorded in
+// that cell on earlier calls (1 point in kOrdSample, halved at each call).
+// Costs map to 16 classes; a counting sort (class-major, hardest first; order
+// inside a class is whatever the atomics give) yields the queue -> point
+// permutation.  Results do not depend on the order: every point is still
+// solved by the same arithmetic on its own.
+//
+// Launches: seed (+ class counts) -> scan (1 block; + folds the previous
+// call's records into the table) -> scatter -> iterate -> angles (+ records,
+// + clears the class counts).  (Doing the one-block steps in the last block of
+// the kernel before, found with a ticket counter, measured 0.6 ms: 4k
+// same-address returning atomics.)
+constexpr int kOrdSegBlocksMin = 16;  // histogram segment: >= 16 blocks of 256 points
+
+__device__ __forceinline__ int goal_cell(const RobotDev &r, d3 g, d3 shoulder) {
+  const double dx = g.x - shoulder.x, dy = g.y - shoulder.y, dz = g.z - shoulder.z;
+  const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+  const double reach = r.links[1] + r.links[2] + r.links[3];
+  int rb = (int)(dist / reach * kOrdCellsR);
+  rb = rb < 0 ? 0 : (rb >= kOrdCellsR ? kOrdCellsR - 1 : rb);
+  int eb = dist > 0.0 ? (int)((dz / dist + 1.0) * (0.5 * kOrdCellsE)) : kOrdCellsE / 2;
+  eb = eb < 0 ? 0 : (eb >= kOrdCellsE ? kOrdCellsE - 1 : eb);
+  return rb * kOrdCellsE + eb;
+}
+
+__device__ __forceinline__ int cost_class(const FabOrderDev *T, int cell, int max_iter) {
+  const unsigned int n = T->cnt[cell];
+  const float mean = n ? (float)T->sum[cell] / (float)n : T->mean;
+  const int k = (int)(mean * kOrdClasses / (float)(max_iter + 1));
+  return k < 0 ? 0 : (k >= kOrdClasses ? kOrdClasses - 1 : k);
+}
+
+// Exclusive scan of the class counts in queue order (hardest class first,
+// then segment), in place: hist becomes the per-(class, segment) cursors the
+// scatter advances.  One block.
+__device__ void order_scan(FabOrderDev *T, int nseg) {
+  __shared__ uint32_t part[256];
+  const int t = threadIdx.x;
+  const int E = kOrdClasses * nseg;
+  const int per = (E + 255) / 256, b0 = t * per, b1 = min(E, b0 + per);
+  // scan position e = class (kOrdClasses-1 - e / nseg), segment e % nseg
+  auto at = [&](int e) { return (kOrdClasses - 1 - e / nseg) * nseg + e % nseg; };
+  uint32_t s = 0;
+  for (int e = b0; e < b1; ++e) s += T->hist[at(e)];
+  part[t] = s;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t v = (t >= d) ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - s;
+  for (int e = b0; e < b1; ++e) {
+    const int k = at(e);
+    const uint32_t c = T->hist[k];
+    T->hist[k] = run;
+    run += c;
+  }
+}
+
+// Fold the records into the halved table and refresh the mean.  One block.
+__device__ void order_fold(FabOrderDev *T) {
+  __shared__ unsigned int ls[kOrdCells], lc[kOrdCells];
+  __shared__ unsigned long long red[2][4];
+  const int t = threadIdx.x;
+  for (int c = t; c < kOrdCells; c += 256) {
+    ls[c] = T->sum[c] >> 1;
+    lc[c] = T->cnt[c] >> 1;
+  }
+  __syncthreads();
+  const unsigned int ns = T->nsample < kOrdMaxSample ? T->nsample : kOrdMaxSample;
+  for (unsigned int k = t; k < ns; k += 256) {
+    const unsigned int v = T->sample[k];
+    atomicAdd(&ls[v >> 16], v & 0xffffu);
+    atomicAdd(&lc[v >> 16], 1u);
+  }
+  __syncthreads();
+  unsigned long long s = 0, n = 0;
+  for (int c = t; c < kOrdCells; c += 256) {
+    T->sum[c] = ls[c];
+    T->cnt[c] = lc[c];
+    s += ls[c];
+    n += lc[c];
+  }
+  s = wave_sum_u64(s);
+  n = wave_sum_u64(n);
+  if ((t & 63) == 0) {
+    red[0][t >> 6] = s;
+    red[1][t >> 6] = n;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const unsigned long long ts = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    const unsigned long long tc = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    T->mean = tc ? (float)((double)ts / (double)tc) : 0.0f;
+    T->nsample = 0;
+  }
+}
+
+// One block: this call's class counts -> cursors, then the previous call's
+// records -> the table (which the next call's seed kernel reads: the table
+// lags one call, which costs nothing but saves a launch).
+__global__ __launch_bounds__(256) void fabrik_order_scan_kernel(FabOrderDev *T, int nseg) {
+  order_scan(T, nseg);
+  __syncthreads();
+  order_fold(T);
+}
+
+template <bool ORD>
 __global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  d3 g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
-  if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
-    atomicMin(&a.S->first_oob, (unsigned long long)i);
-  d3 J[4];
-  int st = seed_pose(a.r, g, J);
-  store_joints(a.seeds, i, J);
-  a.status[i] = (uint8_t)st;
+  __shared__ unsigned int cnt[kOrdClasses];
+  const int t = threadIdx.x;
+  if (ORD) {
+    if (t < kOrdClasses) cnt[t] = 0;
+    __syncthreads();
+  }
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
+  if (i < a.n) {
+    d3 g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
+    if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
+      atomicMin(&a.S->first_oob, (unsigned long long)i);
+    d3 J[4];
+    int st = seed_pose(a.r, g, J);
+    store_joints(a.seeds, i, J);
+    if constexpr (ORD) {
+      a.status_in[i] = (uint8_t)st;
+      const int cell = goal_cell(a.r, g, J[0]);
+      const int k = cost_class(a.ord, cell, a.max_iter);
+      a.cell[i] = (uint16_t)(cell | (k << 10));  // the scatter must see this very class
+      atomicAdd(&cnt[k], 1u);
+    } else {
+      a.status[i] = (uint8_t)st;
+    }
+  }
+  if constexpr (ORD) {
+    __syncthreads();
+    if (t < kOrdClasses && cnt[t])
+      atomicAdd(&a.ord->hist[t * a.nseg + blockIdx.x / a.seg_blocks], cnt[t]);
+  }
+}
+
+// scatter: perm[cursor] = point (one point per lane; one atomic per class
+// and block claims the block's range of each class in its segment)
+__global__ __launch_bounds__(256) void fabrik_order_scatter_kernel(FabArgs a) {
+  __shared__ uint32_t wcnt[4][kOrdClasses], base[kOrdClasses];
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
+  const int k = (i < a.n) ? (a.cell[i] >> 10) : -1;
+  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int rank = 0;
+#pragma unroll
+  for (int c = 0; c < kOrdClasses; ++c) {
+    const unsigned long long m = __ballot(k == c);
+    if (k == c) rank = __popcll(m & lt);
+    if (lane == 0) wcnt[w][c] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  if (t < kOrdClasses) {
+    const uint32_t tot = wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
+    base[t] = tot ? atomicAdd(&a.ord->hist[t * a.nseg + blockIdx.x / a.seg_blocks], tot) : 0u;
+  }
+  __syncthreads();
+  if (k >= 0) {
+    uint32_t pos = base[k] + rank;
+    for (int v = 0; v < w; ++v) pos += wcnt[v][k];
+    a.perm[pos] = (int32_t)i;
+    a.iperm[i] = (int32_t)pos;
+  }
 }
 
 // 2. persistent iteration with per-lane refill.
 // a.chunk: points a wave takes from the global queue at once (tuning knob,
 // IKHIP_FABRIK_CHUNK; small enough that every wave gets work at 1M points).
 
-template <int REFILL_MIN>
+// ORD: the queue is a.perm (work order above): a refilled lane gathers its
+// point's seed pose and goal, and writes its results at its queue position,
+// which the angles kernel maps back to the point.
+template <int REFILL_MIN, bool ORD>
 __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -167,7 +351,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   int64_t qnext = 0, qend = 0;  // wave-uniform: indices not yet handed out
   bool exhausted = false;
   bool active = false;
-  int64_t idx = 0;
+  int64_t idx = 0;  // queue position (= the point index unless ORD)
   d3 J0 = {0, 0, 0}, J1 = J0, J2 = J0, J3 = J0, g = J0;
   double se = 1.0, ge = 1.0;
   int step = 0, st = IK_OK;
@@ -200,10 +384,17 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
       if (mine >= 0) {
         idx = mine;
         d3 Jn[4];
-        load_joints(a.seeds, idx, Jn);
+        if constexpr (ORD) {
+          const int64_t p = a.perm[idx];
+          load_joints(a.seeds, p, Jn);
+          g = {a.pts[3 * p], a.pts[3 * p + 1], a.pts[3 * p + 2]};
+          st = a.status_in[p];
+        } else {
+          load_joints(a.seeds, idx, Jn);
+          g = {a.pts[3 * idx], a.pts[3 * idx + 1], a.pts[3 * idx + 2]};
+          st = a.status[idx];
+        }
         J0 = Jn[0]; J1 = Jn[1]; J2 = Jn[2]; J3 = Jn[3];
-        g = {a.pts[3 * idx], a.pts[3 * idx + 1], a.pts[3 * idx + 2]};
-        st = a.status[idx];
         se = 1.0;
         ge = 1.0;
         step = 0;
@@ -225,35 +416,56 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   }
 }
 
-// 3. angles + stats (uniform work, one point per lane)
+// 3. angles + stats (uniform work, one point per lane).  ORD: the iteration
+// results sit at queue positions (gathered through iperm); 1 in kOrdSample
+// points records (cell, iterations) for the next call's cost table.
+template <bool ORD>
 __global__ __launch_bounds__(256) void fabrik_angles_kernel(FabArgs a) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   bool valid = i < a.n;
   int it = 0;
   if (valid) {
-    int st = a.status[i];
-    it = a.iters[i];
+    const int64_t q = ORD ? (int64_t)a.iperm[i] : i;
+    int st = a.status[q];
+    it = a.iters[q];
+    d3 J[4];
     double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
-    if (st == IK_OK) {
-      d3 J[4];
-      load_joints(a.joints, i, J);
-      get_angles(J, th, st);
-    }
+    if (st == IK_OK || ORD) load_joints(a.joints, q, J);
+    if (st == IK_OK) get_angles(J, th, st);
     if (st != IK_OK) record_error(a.S, i, st);
     double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
     o[0] = make_double2(th[0], th[1]);
     o[1] = make_double2(th[2], th[3]);
+    if constexpr (ORD) {
+      if (a.iters_out) a.iters_out[i] = it;
+      if (a.joints_out) store_joints(a.joints_out, i, J);
+      if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
+        a.ord->sample[i / kOrdSample] =
+            ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) |
+            (uint32_t)(it < 0xffff ? it : 0xffff);
+    }
+  }
+  if constexpr (ORD) {
+    if (i == 0) {
+      const int64_t ns = (a.n + kOrdSample - 1) / kOrdSample;
+      a.ord->nsample = (uint32_t)(ns < kOrdMaxSample ? ns : kOrdMaxSample);
+    }
+    if (i < (int64_t)kOrdClasses * a.nseg) a.ord->hist[i] = 0;  // for the next call
   }
   block_iter_stats(a.S, valid, it, a.max_iter);
 }
 
+static size_t up256(size_t b) { return (b + 255) & ~(size_t)255; }
+
 size_t fabrik_scratch_bytes(int64_t n) {
-  // seeds n*12 doubles, joints n*12 doubles, iters n int32, status n bytes
+  // seeds n*12 doubles, joints n*12 doubles, iters n int32, status n bytes;
+  // work order: perm + iperm n int32 each, cell n uint16, seed status n bytes
   size_t b = 0;
-  b += (size_t)n * 96;
-  b += (size_t)n * 96;
-  b += ((size_t)n * 4 + 255) & ~(size_t)255;
-  b += ((size_t)n + 255) & ~(size_t)255;
+  b += up256((size_t)n * 96);
+  b += up256((size_t)n * 96);
+  b += up256((size_t)n * 4);
+  b += up256((size_t)n);
+  b += 2 * up256((size_t)n * 4) + up256((size_t)n * 2) + up256((size_t)n);
   return b + 1024;
 }
 
@@ -272,7 +484,7 @@ static int num_cus() {
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
-                         int variant) {
+                         int variant, FabOrderDev *ord) {
   if (n <= 0) return;
   FabArgs a;
   a.r = r;
@@ -286,6 +498,15 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   a.joints = joints;
   a.S = S;
   a.chunk = 64;
+  a.perm = nullptr;
+  a.iperm = nullptr;
+  a.status_in = nullptr;
+  a.cell = nullptr;
+  a.ord = ord;
+  a.nseg = 0;
+  a.seg_blocks = 1;
+  a.iters_out = nullptr;
+  a.joints_out = nullptr;
   unsigned grid = (unsigned)((n + 255) / 256);
   if (variant == 0) {
     a.seeds = nullptr;
@@ -297,17 +518,48 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   }
   char *p = static_cast<char *>(scratch);
   a.seeds = reinterpret_cast<double *>(p);
-  p += (size_t)n * 96;
+  p += up256((size_t)n * 96);
   double *jtmp = reinterpret_cast<double *>(p);
-  p += (size_t)n * 96;
+  p += up256((size_t)n * 96);
   int32_t *itmp = reinterpret_cast<int32_t *>(p);
-  p += ((size_t)n * 4 + 255) & ~(size_t)255;
+  p += up256((size_t)n * 4);
   a.status = reinterpret_cast<uint8_t *>(p);
-  if (!a.joints) a.joints = jtmp;
-  if (!a.iters) a.iters = itmp;
-  kt_begin("fabrik_seed_kernel", stream);
-  hipLaunchKernelGGL(fabrik_seed_kernel, dim3(grid), dim3(256), 0, stream, a);
-  kt_end(stream);
+  p += up256((size_t)n);
+  static const int order_on = env_int("IKHIP_FABRIK_ORDER", 1);
+  const bool ordered = ord && order_on && n < (int64_t)1 << 31;
+  if (ordered) {
+    // iteration results land at queue positions in scratch; the angles kernel
+    // gathers them back to point order into the caller's (nullable) buffers
+    a.perm = reinterpret_cast<int32_t *>(p);
+    p += up256((size_t)n * 4);
+    a.iperm = reinterpret_cast<int32_t *>(p);
+    p += up256((size_t)n * 4);
+    a.cell = reinterpret_cast<uint16_t *>(p);
+    p += up256((size_t)n * 2);
+    a.status_in = reinterpret_cast<uint8_t *>(p);
+    a.seg_blocks = (int)((grid + kOrdMaxSeg - 1) / kOrdMaxSeg);
+    if (a.seg_blocks < kOrdSegBlocksMin) a.seg_blocks = kOrdSegBlocksMin;
+    a.nseg = (int)((grid + a.seg_blocks - 1) / a.seg_blocks);
+    a.iters_out = a.iters;
+    a.joints_out = a.joints;
+    a.iters = itmp;
+    a.joints = jtmp;
+    kt_begin("fabrik_seed_kernel", stream);
+    hipLaunchKernelGGL(fabrik_seed_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
+    kt_end(stream);
+    kt_begin("fabrik_order_scan_kernel", stream);
+    hipLaunchKernelGGL(fabrik_order_scan_kernel, dim3(1), dim3(256), 0, stream, ord, a.nseg);
+    kt_end(stream);
+    kt_begin("fabrik_order_scatter_kernel", stream);
+    hipLaunchKernelGGL(fabrik_order_scatter_kernel, dim3(grid), dim3(256), 0, stream, a);
+    kt_end(stream);
+  } else {
+    if (!a.joints) a.joints = jtmp;
+    if (!a.iters) a.iters = itmp;
+    kt_begin("fabrik_seed_kernel", stream);
+    hipLaunchKernelGGL(fabrik_seed_kernel<false>, dim3(grid), dim3(256), 0, stream, a);
+    kt_end(stream);
+  }
   // persistent grid: blocks_per_cu 256-thread blocks per CU (= waves per SIMD)
   // measured on MI355X at 1M points (tools/sweep_fabrik.py): 2 blocks/CU with
   // 64-point grabs beats 4 and 8 (more lanes = fewer points per lane = a
@@ -320,14 +572,25 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   if ((int64_t)pgrid * 4 > waves_needed)
     pgrid = (unsigned)((waves_needed + 3) / 4 > 0 ? (waves_needed + 3) / 4 : 1);
   kt_begin("fabrik_iter_kernel", stream);
-  if (variant == 2)
-    hipLaunchKernelGGL(fabrik_iter_kernel<1>, dim3(pgrid), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL(fabrik_iter_kernel<8>, dim3(pgrid), dim3(256), 0, stream, a);
+  if (variant == 2) {
+    if (ordered)
+      hipLaunchKernelGGL((fabrik_iter_kernel<1, true>), dim3(pgrid), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((fabrik_iter_kernel<1, false>), dim3(pgrid), dim3(256), 0, stream, a);
+  } else {
+    if (ordered)
+      hipLaunchKernelGGL((fabrik_iter_kernel<8, true>), dim3(pgrid), dim3(256), 0, stream, a);
+    else
+      hipLaunchKernelGGL((fabrik_iter_kernel<8, false>), dim3(pgrid), dim3(256), 0, stream, a);
+  }
   kt_end(stream);
   kt_begin("fabrik_angles_kernel", stream);
-  hipLaunchKernelGGL(fabrik_angles_kernel, dim3(grid), dim3(256), 0, stream, a);
+  if (ordered)
+    hipLaunchKernelGGL(fabrik_angles_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(fabrik_angles_kernel<false>, dim3(grid), dim3(256), 0, stream, a);
   kt_end(stream);
+
 }
 
 // ------------------------------------------------------ Fabrik.calculate ----

@@ -278,6 +278,32 @@ def test_ann_dropin_api():
     assert p.shape == (1, 4) and p.dtype == np.float32
 
 
+def test_fabrik_work_order_is_invisible():
+    """The hard-first work order (ik_fabrik.hip "Work order") only changes which
+    point a lane takes when: results are bit-identical from call to call while
+    the cost table learns, across batch sizes with different histogram segment
+    counts, and iteration counts stay equal to the oracle's."""
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    c = _native.Context(0)
+    try:
+        big = random_dist(60_000, seed=5)
+        first = None
+        for n in (60_000, 9_000, 60_000, 300, 60_000):
+            ang, it, _, _ = c.fabrik_solve(big[:n], 1e-3, 100)
+            if n == 60_000:
+                if first is None:
+                    first = (ang.copy(), it.copy())
+                else:
+                    assert np.array_equal(ang, first[0], equal_nan=True)
+                    assert np.array_equal(it, first[1])
+        ref_ang, ref_it, _, _ = O.fabrik_ikine(big[:8192], 1e-3, 100)
+        assert np.array_equal(first[1][:8192], ref_it)  # bit-exact iteration counts
+        assert np.abs(first[0][:8192] - ref_ang).max() <= 1e-9
+    finally:
+        c.close()
+
+
 def test_device_pointer_path(ctx1):
     import torch
     from inversekinematicsann_amd import _native

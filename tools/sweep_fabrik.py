@@ -36,7 +36,13 @@ def run(env, n, tol, mi):
 
 if __name__ == "__main__":
     cases = []
-    for var in ("1", "2", "0"):
+    if len(sys.argv) > 1 and sys.argv[1] == "order":  # work order on/off x grid knobs
+        for order in ("0", "1"):
+            for bpc in ("2", "4"):
+                for chunk in ("32", "64"):
+                    cases.append({"IKHIP_FABRIK_ORDER": order, "IKHIP_FABRIK_BPC": bpc,
+                                  "IKHIP_FABRIK_CHUNK": chunk})
+    for var in (() if cases else ("1", "2", "0")):
         for bpc in ("2", "4", "8"):
             for chunk in ("64", "256"):
                 if var == "0" and (bpc != "8" or chunk != "64"):
@@ -46,4 +52,5 @@ if __name__ == "__main__":
     for n, tol, mi in ((1_000_000, 1e-3, 100), (1_000_000, 1e-5, 200)):
         for c in cases:
             r = run(c, n, tol, mi)
-            print(json.dumps({"n": n, "tol": tol, **c, **r}), flush=True)
+            tot = sum(v for v in r.values() if isinstance(v, float))
+            print(json.dumps({"n": n, "tol": tol, **c, "total_ms": tot, **r}), flush=True)
