@@ -42,10 +42,11 @@ struct d3 {
 // The reference's pow(v, 2).
 __device__ __forceinline__ double sq(double v) { return v * v; }
 
-// kinematics/point.py:25-29 get_distance_between
-__device__ __forceinline__ double dist3(d3 a, d3 b) {
-  return sqrt(sq(a.x - b.x) + sq(a.y - b.y) + sq(a.z - b.z));
+// kinematics/point.py:25-29 get_distance_between, and its radicand
+__device__ __forceinline__ double dist3_sq(d3 a, d3 b) {
+  return sq(a.x - b.x) + sq(a.y - b.y) + sq(a.z - b.z);
 }
+__device__ __forceinline__ double dist3(d3 a, d3 b) { return sqrt(dist3_sq(a, b)); }
 
 __device__ __forceinline__ void set_err(int &st, int code) {
   if (st == IK_OK) st = code;

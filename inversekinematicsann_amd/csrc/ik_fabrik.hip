@@ -13,6 +13,8 @@
 //    lane) -> angles_kernel (law of cosines + per-batch stats).
 //  * simple: everything in one kernel, one point per lane, no refill.
 // Per point the state is 4 joints + goal (15 doubles) held in VGPRs.
+#include <cmath>
+
 #include "ik_common.h"
 
 namespace ikhip {
@@ -20,17 +22,37 @@ namespace ikhip {
 // One FABRIK iteration for the 4-joint chain (fabrik.py:57-64): backward pass
 // from the goal (dists[2], dists[1], dists[0]), start error, forward pass from
 // the start (dists[1], dists[2], dists[3]), goal error.  cur[0] is always start.
+// The two errors are returned SQUARED (the radicands of get_distance_between):
+// they are only compared with tol (fabrik.py:57), and sqrt(x) > tol <=> x > t
+// for t = tol_threshold(tol) exactly, sqrt being correctly rounded and monotonic.
 __device__ __forceinline__ void fabrik_step4(const d3 start, d3 &c1, d3 &c2, d3 &c3,
-                                             const d3 g, const double *L, double &se,
-                                             double &ge, int &st) {
+                                             const d3 g, const double *L, double &se2,
+                                             double &ge2, int &st) {
   d3 b2 = point_between(g, c2, L[2], st);
   d3 b1 = point_between(b2, c1, L[1], st);
   d3 b0 = point_between(b1, start, L[0], st);
-  se = dist3(b0, start);
+  se2 = dist3_sq(b0, start);
   c1 = point_between(start, b1, L[1], st);
   c2 = point_between(c1, b2, L[2], st);
   c3 = point_between(c2, g, L[3], st);
-  ge = dist3(c3, g);
+  ge2 = dist3_sq(c3, g);
+}
+
+// The largest x with fl(sqrt(x)) <= tol (NaN for a NaN tol, -inf for a
+// negative one), so that the reference's `sqrt(x) > tol` is `x > t` bit for
+// bit.  The loop's initial errors of 1.0 stay 1.0 (sqrt(1) = 1 exactly).
+static double tol_threshold(double tol) {
+  if (std::isnan(tol)) return NAN;
+  if (tol < 0) return -INFINITY;
+  if (std::isinf(tol)) return INFINITY;
+  double t = tol * tol;
+  while (std::sqrt(t) > tol) t = std::nextafter(t, -INFINITY);
+  for (;;) {
+    const double u = std::nextafter(t, INFINITY);
+    if (std::sqrt(u) <= tol) t = u;
+    else break;
+  }
+  return t;
 }
 
 // kinematics/inverse.py:54-112 __get_angles; J = FABRIK joints B, C, D, E.
@@ -90,7 +112,8 @@ struct FabArgs {
   RobotDev r;
   const double *pts;
   int64_t n;
-  double tol;
+  double tol;      // fabrik.py:57 err_margin, as given
+  double tol2;     // tol_threshold(tol): the loop compares squared errors with it
   int max_iter;
   int check_limits;
   double *ang;
@@ -129,7 +152,7 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
     int st = seed_pose(a.r, g, J);
     double se = 1.0, ge = 1.0;
     if (st == IK_OK) {
-      while (((se > a.tol) || (ge > a.tol)) && (a.max_iter > it)) {
+      while (((se > a.tol2) || (ge > a.tol2)) && (a.max_iter > it)) {
         fabrik_step4(J[0], J[1], J[2], J[3], g, a.r.links, se, ge, st);
         ++it;
         if (st != IK_OK) break;
@@ -344,7 +367,7 @@ template <int REFILL_MIN, bool ORD>
 __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const double tol = a.tol;
+  const double tol2 = a.tol2;
   const int max_iter = a.max_iter;
   double L[4] = {a.r.links[0], a.r.links[1], a.r.links[2], a.r.links[3]};
 
@@ -402,7 +425,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
       }
     }
     if (active) {
-      if (st == IK_OK && ((se > tol) || (ge > tol)) && (max_iter > step)) {
+      if (st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step)) {
         fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
         ++step;
       } else {
@@ -491,6 +514,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   a.pts = pts;
   a.n = n;
   a.tol = tol;
+  a.tol2 = tol_threshold(tol);
   a.max_iter = max_iter;
   a.check_limits = check_limits ? 1 : 0;
   a.ang = ang;
@@ -598,7 +622,7 @@ template <int NJ>
 __global__ __launch_bounds__(256) void fabrik_calc_kernel(const double *dists_in,
                                                           const double *init, int shared,
                                                           const double *goals, int64_t n,
-                                                          double tol, int max_iter,
+                                                          double tol2, int max_iter,
                                                           double *joints, int32_t *iters,
                                                           DevStats *S) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -616,15 +640,15 @@ __global__ __launch_bounds__(256) void fabrik_calc_kernel(const double *dists_in
     const d3 start = cur[0];
     double se = 1.0, ge = 1.0;
     int st = IK_OK;
-    while (((se > tol) || (ge > tol)) && (max_iter > it)) {
+    while (((se > tol2) || (ge > tol2)) && (max_iter > it)) {  // squared errors
       B[NJ - 1] = g;
 #pragma unroll
       for (int k = NJ - 2; k >= 0; --k) B[k] = point_between(B[k + 1], cur[k], L[k], st);
-      se = dist3(B[0], start);
+      se = dist3_sq(B[0], start);
       cur[0] = start;
 #pragma unroll
       for (int k = 1; k < NJ; ++k) cur[k] = point_between(cur[k - 1], B[k], L[k], st);
-      ge = dist3(cur[NJ - 1], g);
+      ge = dist3_sq(cur[NJ - 1], g);
       ++it;
       if (st != IK_OK) break;
     }
@@ -647,10 +671,11 @@ void launch_fabrik_calc(int nj, const double *dists, const double *init, bool in
   if (n <= 0) return;
   unsigned grid = (unsigned)((n + 255) / 256);
   int sh = init_shared ? 1 : 0;
+  const double tol2 = tol_threshold(tol);
 #define IK_CALC_CASE(K)                                                                      \
   case K:                                                                                    \
     hipLaunchKernelGGL(fabrik_calc_kernel<K>, dim3(grid), dim3(256), 0, st, dists, init, sh, \
-                       goals, n, tol, max_iter, joints, iters, S);                           \
+                       goals, n, tol2, max_iter, joints, iters, S);                          \
     break;
   kt_begin("fabrik_calc_kernel", st);
   switch (nj) {
