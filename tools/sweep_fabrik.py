@@ -42,6 +42,9 @@ if __name__ == "__main__":
                 for chunk in ("32", "64"):
                     cases.append({"IKHIP_FABRIK_ORDER": order, "IKHIP_FABRIK_BPC": bpc,
                                   "IKHIP_FABRIK_CHUNK": chunk})
+    if len(sys.argv) > 1 and sys.argv[1] == "grid":  # persistent-grid size, ordered pipeline
+        for bpc in ("2", "3", "4"):
+            cases.append({"IKHIP_FABRIK_BPC": bpc})
     for var in (() if cases else ("1", "2", "0")):
         for bpc in ("2", "4", "8"):
             for chunk in ("64", "256"):
