@@ -65,10 +65,18 @@ def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; IKHIP_DIST_BACKEND=gloo + more ranks than GPUs is only for
+    # rehearsing the N > 1 bookkeeping on a one-GPU box (ranks share device 0)
+    backend = os.environ.get("IKHIP_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if "WORLD_SIZE" in os.environ:  # launched by torch.distributed.run (any N)
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -101,6 +109,10 @@ def sum_over_ranks(v: float, world: int) -> float:
     t = torch.tensor([v], dtype=torch.float64, device="cuda")
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+def _pts(n: int) -> str:
+    return f"{n // 1_000_000}M" if n % 1_000_000 == 0 else f"{n}"
 
 
 def load_traffic(path, kernel):
@@ -172,12 +184,12 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
     if mode == "fp32":
         res["dtype"] = "fp32"
         res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
-                           "1M random_dist points per GPU")
+                           f"{_pts(n)} random_dist points per GPU")
     else:
         res["dtype"] = "fp32 via bf16x6 (3-way bf16 split, 6 MFMA products, fp32 accumulate)"
         res["workload"] = ("ANN MLP forward (3-12x500tanh-4), hidden GEMMs in the bf16x6 mode "
                            "(fp32-accurate: tests/test_gpu_parity.py::test_ann_bf16x6_mode) + "
-                           "fused FK round-trip error, 1M random_dist points per GPU")
+                           f"fused FK round-trip error, {_pts(n)} random_dist points per GPU")
     return res
 
 
@@ -213,7 +225,7 @@ def run_fabrik(ctx, dpts, n, args, world):
                        "iterations_per_launch": int(st.sum_iters)}
     res["dtype"] = "f64"
     res["workload"] = (f"FABRIK ikine (seed FK + loop + angles), tol {args.tol:g} / "
-                       f"{args.max_iter} iterations, float64, 1M random_dist points per GPU")
+                       f"{args.max_iter} iterations, float64, {_pts(n)} random_dist points per GPU")
     return res
 
 
