@@ -128,9 +128,13 @@ int ik_ann_solve(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *
  * CPU float32 forward.  IK_ANN_BF16X6: every fp32 operand split into three bf16
  * parts and six bf16 MFMA products accumulated in fp32 -- fp32-level accuracy
  * (tested within 1e-6 of a float64 forward, the fp32 mode's own distance from
- * it) at ~2.7x the MFMA rate.  The input layer and a one-tile output layer stay
- * fp32 in both modes.  Environment default: IKHIP_ANN_MODE=bf16x6. */
-enum { IK_ANN_FP32 = 0, IK_ANN_BF16X6 = 1 };
+ * it) at ~2.7x the MFMA rate.  IK_ANN_FP16X3: two fp16 parts (weights
+ * pre-scaled by a power of two) and three fp16 MFMA products, on layers whose
+ * input is tanh/sigmoid-bounded (others stay fp32); as close to a float64
+ * forward as numpy's float32 one on the tested networks, at ~5x the MFMA rate.
+ * The input layer and a one-tile output layer stay fp32 in every mode.
+ * Environment default: IKHIP_ANN_MODE=bf16x6|fp16x3. */
+enum { IK_ANN_FP32 = 0, IK_ANN_BF16X6 = 1, IK_ANN_FP16X3 = 2 };
 int ik_ann_set_mode(ik_ctx *ctx, int mode);
 int ik_ann_get_mode(ik_ctx *ctx); /* the mode, or -ik_status */
 

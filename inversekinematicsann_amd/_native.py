@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_fabrik_solve", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode")
-ANN_MODES = {"fp32": 0, "bf16x6": 1}
+ANN_MODES = {"fp32": 0, "bf16x6": 1, "fp16x3": 2}
 
 
 class NativeUnavailable(RuntimeError):
@@ -251,7 +251,7 @@ class Context:
                                          *[_ptr(v) for v in sc]))
 
     def ann_set_mode(self, mode: str):
-        """Hidden-layer GEMM arithmetic: "fp32" (default) or "bf16x6" (ikhip.h)."""
+        """Hidden-layer GEMM arithmetic: "fp32" (default), "bf16x6" or "fp16x3" (ikhip.h)."""
         if mode not in ANN_MODES:
             raise ValueError(f"unknown ANN mode {mode!r}; expected one of {sorted(ANN_MODES)}")
         self._check(self.lib.ik_ann_set_mode(self.handle, ANN_MODES[mode]))

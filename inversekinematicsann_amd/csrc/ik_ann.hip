@@ -345,15 +345,142 @@ __device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__res
   if (g + 1 < G16) step_x<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
 }
 
-// One Dense layer for a wave with NR column tiles.  wx: the layer's split-bf16
-// weight planes (bf16x6 mode, full-width layers only), else nullptr.
+// ------------------------------------------------- split-fp16 (fp16x3) mode ----
+// Opt-in (IK_ANN_FP16X3): x = hi + lo in fp16 (round to nearest; the residual
+// is exact in fp32), weights pre-scaled by 2^k so their largest is ~2^14, and
+// the three products above 2^-22 -- lo*hi, hi*lo, hi*hi -- accumulated in fp32
+// by v_mfma_f32_32x32x16_f16 (fp16 products are exact in fp32); the result is
+// scaled back by 2^-k (exact).  3 MFMAs (96 cycles) per 32x32x16 block against
+// 6 for bf16x6 and 8 fp32 ones (512 cycles), 4 B per weight from L2.  Only for
+// layers whose input is bounded (the layer before is tanh or sigmoid): fp16's
+// range ends at 65504.  Accuracy on the reference architecture: max |d| to a
+// float64 forward 3.6e-7, the same as numpy's float32 forward (test_gpu_parity).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+struct Split2 {
+  f16x8 hi, lo;
+};
+
+__device__ __forceinline__ Split2 split2h(f32x8 x) {
+  Split2 s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 v = {x[2 * i], x[2 * i + 1]};
+    const f16x2 h = __builtin_convertvector(v, f16x2);
+    const f32x2 r = v - __builtin_convertvector(h, f32x2);
+    const f16x2 l = __builtin_convertvector(r, f16x2);
+    s.hi[2 * i] = h[0];
+    s.hi[2 * i + 1] = h[1];
+    s.lo[2 * i] = l[0];
+    s.lo[2 * i + 1] = l[1];
+  }
+  return s;
+}
+
+// weight planes of one K step: plane p (0 hi, 1 lo) of step g of column tile
+// nt is block (nt * G16 + g) * 2 + p of 64 lanes x 16 B
+template <int NR>
+struct WStepH {
+  f16x8 p[NR][2];
+};
+
+template <int NR>
+__device__ __forceinline__ void load_wh(WStepH<NR> &w, const f16x8 *const (&bp)[NR], int g) {
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int p = 0; p < 2; ++p) w.p[j][p] = bp[j][((size_t)g * 2 + p) * 64];
+}
+
+// One K step (see step_x): weights of step g+2 and A of step g+1 in the shadow
+// of the 3 * MR * NR MFMAs of step g.
 template <int MR, int NR>
+__device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WStepH<NR> &fill,
+                                       const f16x8 *const (&bp)[NR], const float *ap, int g,
+                                       int last, f32x16 (&acc)[MR][NR]) {
+  __builtin_amdgcn_sched_barrier(0);
+  load_wh(fill, bp, min(g + 2, last));
+  f32x8 an[MR];
+  load_a(an, ap, min(g + 1, last));
+  Split2 sn[MR];
+#pragma unroll
+  for (int m = 0; m < MR; ++m) sn[m] = split2h(an[m]);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      f32x16 c = acc[m][j];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[m].lo, w.p[j][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[m].hi, w.p[j][1], c, 0, 0, 0);
+      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[m].hi, w.p[j][0], c, 0, 0, 0);
+    }
+  constexpr int kMfma = 3 * MR * NR, kLead = (kMfma >= 12) ? 6 : kMfma / 2;
+  __builtin_amdgcn_sched_group_barrier(0x020, 2 * NR, 0);  // VMEM reads
+  __builtin_amdgcn_sched_group_barrier(0x100, 2 * MR, 0);  // DS reads
+  __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
+#pragma unroll
+  for (int i = 0; i < kMfma - kLead; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int m = 0; m < MR; ++m) sa[m] = sn[m];
+}
+
+// Full-width layer in fp16x3 mode; the accumulators come back scaled by xinv.
+template <int MR, int NR>
+__device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__restrict__ wx,
+                                             int G16, float xinv, int wave, int lane,
+                                             f32x16 (&acc)[MR][NR]) {
+  const int r = lane & 31, h = lane >> 5;
+  const float *ap = H + r * kLd + 8 * h;
+  const f16x8 *bp[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    bp[j] = wx + (size_t)(wave + kWaves * j) * G16 * 2 * 64 + lane;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
+  }
+  const int last = G16 - 1;
+  WStepH<NR> w0, w1, w2;
+  load_wh(w0, bp, 0);
+  load_wh(w1, bp, min(1, last));
+  Split2 sa[MR];
+  {
+    f32x8 a0[MR];
+    load_a(a0, ap, 0);
+#pragma unroll
+    for (int m = 0; m < MR; ++m) sa[m] = split2h(a0[m]);
+  }
+  int g = 0;
+  for (; g + 3 <= G16; g += 3) {
+    step_h<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
+    step_h<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
+    step_h<MR, NR>(sa, w2, w1, bp, ap, g + 2, last, acc);
+  }
+  if (g < G16) step_h<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
+  if (g + 1 < G16) step_h<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j) acc[m][j] *= xinv;
+}
+
+// One Dense layer for a wave with NR column tiles.  X: 0 fp32, 1 bf16x6,
+// 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
+// a layer that stays fp32.
+template <int MR, int NR, int X = 0>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wave, int lane, unsigned long long *st,
-                                          const bf16x8 *wx = nullptr, int G16 = 0) {
+                                          const void *wx = nullptr, int G16 = 0,
+                                          float xinv = 1.0f) {
   f32x16 acc[MR][NR];
-  if (wx)
-    layer_gemm_x<MR, NR>(H, wx, G16, wave, lane, acc);
+  if (X == 1 && wx)
+    layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, wave, lane, acc);
+  else if (X == 2 && wx)
+    layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, xinv, wave, lane, acc);
   else
     layer_gemm<MR, NR>(H, wp, G, 0, G, wave, kWaves, lane, acc);
   switch (act) {
@@ -436,9 +563,10 @@ __device__ __forceinline__ double fk_error(const double *jc, const double th[4],
   return ok ? dist3(e, p) : __builtin_nan("");
 }
 
-// X: bf16x6 mode -- layers whose split weight planes exist (a.m.wx[l]) take
-// the split-bf16 GEMM; the others (input layer, split-K output layer) stay fp32.
-template <int MR, bool X>
+// X: 0 fp32; 1 bf16x6, 2 fp16x3 -- layers whose split weight operand exists
+// (a.m.wx[l]) take the split GEMM; the others (input layer, split-K output
+// layer, fp16x3-ineligible layers) stay fp32.
+template <int MR, int X>
 __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnArgs a) {
   constexpr int BM = 32 * MR;
   __shared__ __attribute__((aligned(16))) float H[BM * kLd];
@@ -484,17 +612,18 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
       const float *bias = a.m.bias[l];
       const int act = a.m.act[l];
       unsigned long long *sl = (stp && l < 14) ? stp + 2 + 2 * l : nullptr;
-      const bf16x8 *wx = X ? reinterpret_cast<const bf16x8 *>(a.m.wx[l]) : nullptr;
+      const void *wx = X ? a.m.wx[l] : nullptr;
       if (NT == 1) {
         run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid, sl);
       } else if (X && wx) {
+        const float xinv = a.m.xinv[l];
         const int G16 = (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
-          case 3: run_layer<MR, 3>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
-          case 2: run_layer<MR, 2>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
-          case 1: run_layer<MR, 1>(H, wp, bias, act, G, wave, lane, sl, wx, G16); break;
+          case 4: run_layer<MR, 4, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
+          case 3: run_layer<MR, 3, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
+          case 2: run_layer<MR, 2, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
+          case 1: run_layer<MR, 1, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
           default: __syncthreads(); break;
         }
       } else {
@@ -555,7 +684,7 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
 // (ik_ann_x.hip defines IKHIP_ANN_X_TU and includes this file): in one module
 // with the fp32 kernel they change the latter's register allocation (29 -> 51
 // spilled VGPRs at MR = 2, -Rpass-analysis=kernel-resource-usage).
-void launch_ann_kernel_x(int mr, unsigned grid, hipStream_t st, const AnnArgs &a);
+void launch_ann_kernel_x(int mr, int xmode, unsigned grid, hipStream_t st, const AnnArgs &a);
 
 #ifndef IKHIP_ANN_X_TU
 
@@ -631,6 +760,49 @@ void ann_pack_layer_x(const float *W, int k, int n, void *dst) {
         }
 }
 
+size_t ann_h_bytes(int k, int n) {
+  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
+  return (size_t)k16 * np * 4;
+}
+
+// The power of two that brings the layer's largest |weight| to [2^13, 2^14):
+// the fp16 planes then keep their full 11 bits down to weights ~2^-10 of the
+// largest, and nothing comes near fp16's 65504.
+int ann_h_scale_exp(const float *W, int k, int n) {
+  float mx = 0.0f;
+  for (size_t i = 0; i < (size_t)k * n; ++i) mx = std::fmax(mx, std::fabs(W[i]));
+  if (!(mx > 0.0f) || !std::isfinite(mx)) return 0;
+  int e = 0;
+  std::frexp(mx, &e);  // mx in [2^(e-1), 2^e)
+  int s = 14 - e;
+  return s < -60 ? -60 : (s > 60 ? 60 : s);
+}
+
+// The fp16x3 weight operand: planes p (0 hi, 1 lo) of W * 2^scale_exp in the
+// B-fragment order of v_mfma_f32_32x32x16_f16 (the bf16x6 layout with two
+// planes): dst[(((nt*G16 + g)*2 + p)*64 + l)*8 + j] = plane p of
+// W[16g + 8*(l>>5) + j][32nt + (l&31)] * 2^scale_exp, each plane rounded to
+// nearest (the scaled weight and its residual are exact in fp32).
+void ann_pack_layer_h(const float *W, int k, int n, int scale_exp, void *dst) {
+  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
+  int G16 = k16 / 16, NT = np / 32;
+  _Float16 *d = static_cast<_Float16 *>(dst);
+  for (int nt = 0; nt < NT; ++nt)
+    for (int g = 0; g < G16; ++g)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int kk = 16 * g + 8 * (lane >> 5) + j;
+          const int c = nt * 32 + (lane & 31);
+          const float x =
+              (kk < k && c < n) ? std::ldexp(W[(size_t)kk * n + c], scale_exp) : 0.0f;
+          const _Float16 h = (_Float16)x;
+          const _Float16 lo = (_Float16)(x - (float)h);
+          const size_t base = (((size_t)nt * G16 + g) * 2) * 64 * 8 + (size_t)lane * 8 + j;
+          d[base] = h;
+          d[base + 64 * 8] = lo;
+        }
+}
+
 static int ann_tile_rows() {
   static int mr = 0;
   if (mr == 0) {
@@ -680,23 +852,29 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);
   bool x = false;
   for (int l = 0; l < m.n_layers; ++l) x = x || m.wx[l] != nullptr;
-  kt_begin(x ? "ann_fused_kernel_bf16x6" : "ann_fused_kernel", st);
-  if (x)
-    launch_ann_kernel_x(mr, grid, st, a);
+  const int xmode = x ? m.xmode : 0;
+  kt_begin(xmode == 1 ? "ann_fused_kernel_bf16x6"
+                      : xmode == 2 ? "ann_fused_kernel_fp16x3" : "ann_fused_kernel",
+           st);
+  if (xmode)
+    launch_ann_kernel_x(mr, xmode, grid, st, a);
   else if (mr == 2)
-    hipLaunchKernelGGL((ann_fused_kernel<2, false>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ann_fused_kernel<2, 0>), dim3(grid), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((ann_fused_kernel<1, false>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ann_fused_kernel<1, 0>), dim3(grid), dim3(256), 0, st, a);
   kt_end(st);
 }
 
 #else  // IKHIP_ANN_X_TU
 
-void launch_ann_kernel_x(int mr, unsigned grid, hipStream_t st, const AnnArgs &a) {
-  if (mr == 2)
-    hipLaunchKernelGGL((ann_fused_kernel<2, true>), dim3(grid), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL((ann_fused_kernel<1, true>), dim3(grid), dim3(256), 0, st, a);
+void launch_ann_kernel_x(int mr, int xmode, unsigned grid, hipStream_t st, const AnnArgs &a) {
+#define IK_X(M, X) hipLaunchKernelGGL((ann_fused_kernel<M, X>), dim3(grid), dim3(256), 0, st, a)
+  if (mr == 2) {
+    if (xmode == 2) IK_X(2, 2); else IK_X(2, 1);
+  } else {
+    if (xmode == 2) IK_X(1, 2); else IK_X(1, 1);
+  }
+#undef IK_X
 }
 
 #endif  // IKHIP_ANN_X_TU

@@ -77,6 +77,8 @@ struct ik_ctx {
   AnnModelDev ann;
   void *ann_buf = nullptr;
   const void *ann_wx[kAnnMaxLayers] = {};  // bf16x6 weight operand of each layer (or null)
+  const void *ann_wh[kAnnMaxLayers] = {};  // fp16x3 weight operand of each layer (or null)
+  float ann_hinv[kAnnMaxLayers] = {};      // fp16x3: 2^-(weight pre-scale exponent)
   int ann_mode = IK_ANN_FP32;
   int fabrik_variant = 1;
   KTimer kt;
@@ -199,7 +201,9 @@ int ik_ctx_create(int device, ik_ctx **out) {
   std::memcpy(c->robot.lim, kDefaultLimits, sizeof(kDefaultLimits));
   if (const char *v = std::getenv("IKHIP_FABRIK_VARIANT")) c->fabrik_variant = std::atoi(v);
   if (const char *v = std::getenv("IKHIP_ANN_MODE"))
-    if (std::strcmp(v, "bf16x6") == 0) c->ann_mode = IK_ANN_BF16X6;
+    c->ann_mode = std::strcmp(v, "bf16x6") == 0   ? IK_ANN_BF16X6
+                  : std::strcmp(v, "fp16x3") == 0 ? IK_ANN_FP16X3
+                                                  : IK_ANN_FP32;
   *out = c;
   return IK_OK;
 }
@@ -484,8 +488,13 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   // one device buffer: per layer packed weights, padded bias and -- for the
   // hidden layers that can take the bf16x6 mode (not the input layer, not a
   // single-column-tile output layer) -- the split bf16 planes
-  std::vector<size_t> woff(n_layers), boff(n_layers), xoff(n_layers, 0);
+  std::vector<size_t> woff(n_layers), boff(n_layers), xoff(n_layers, 0), hoff(n_layers, 0);
+  std::vector<int> hexp(n_layers, 0);
   auto splittable = [&](int l) { return l > 0 && (dims[l + 1] + 31) / 32 > 1; };
+  // fp16x3 also needs a bounded layer input: the layer before is tanh or sigmoid
+  auto halvable = [&](int l) {
+    return splittable(l) && (acts[l - 1] == IK_ACT_TANH || acts[l - 1] == IK_ACT_SIGMOID);
+  };
   size_t total = 0;
   for (int l = 0; l < n_layers; ++l) {
     woff[l] = total;
@@ -499,6 +508,11 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
       total += ann_x_bytes(dims[l], dims[l + 1]);
       total = (total + 255) & ~(size_t)255;
     }
+    if (halvable(l)) {
+      hoff[l] = total;
+      total += ann_h_bytes(dims[l], dims[l + 1]);
+      total = (total + 255) & ~(size_t)255;
+    }
   }
   std::vector<char> host(total, 0);
   for (int l = 0; l < n_layers; ++l) {
@@ -506,6 +520,10 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
     std::memcpy(&host[boff[l]], b[l], (size_t)dims[l + 1] * 4);
     if (splittable(l))
       ann_pack_layer_x(W[l], dims[l], dims[l + 1], &host[xoff[l]]);
+    if (halvable(l)) {
+      hexp[l] = ann_h_scale_exp(W[l], dims[l], dims[l + 1]);
+      ann_pack_layer_h(W[l], dims[l], dims[l + 1], hexp[l], &host[hoff[l]]);
+    }
   }
   IK_HIP(hipStreamSynchronize(c->stream));
   if (c->ann_buf) IK_HIP(hipFree(c->ann_buf));
@@ -524,6 +542,8 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
     m.wp[l] = reinterpret_cast<const float4 *>(base + woff[l]);
     m.bias[l] = reinterpret_cast<const float *>(base + boff[l]);
     c->ann_wx[l] = splittable(l) ? base + xoff[l] : nullptr;
+    c->ann_wh[l] = halvable(l) ? base + hoff[l] : nullptr;
+    c->ann_hinv[l] = std::ldexp(1.0f, -hexp[l]);
   }
   for (int i = 0; i < 3; ++i) {
     m.xm[i] = x_mean[i];
@@ -539,7 +559,7 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
 
 int ik_ann_set_mode(ik_ctx *c, int mode) {
   if (!c) return fail(IK_E_BADARG, "ik_ann_set_mode: NULL context");
-  if (mode != IK_ANN_FP32 && mode != IK_ANN_BF16X6)
+  if (mode != IK_ANN_FP32 && mode != IK_ANN_BF16X6 && mode != IK_ANN_FP16X3)
     return fail(IK_E_BADARG, "ik_ann_set_mode: unknown mode");
   c->ann_mode = mode;
   return IK_OK;
@@ -572,8 +592,13 @@ int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk
   }
   launch_reset_stats(c->d_stats, c->stream);
   AnnModelDev m = c->ann;
-  for (int l = 0; l < m.n_layers; ++l)
-    m.wx[l] = (c->ann_mode == IK_ANN_BF16X6) ? c->ann_wx[l] : nullptr;
+  m.xmode = c->ann_mode;
+  for (int l = 0; l < m.n_layers; ++l) {
+    m.wx[l] = c->ann_mode == IK_ANN_BF16X6   ? c->ann_wx[l]
+              : c->ann_mode == IK_ANN_FP16X3 ? c->ann_wh[l]
+                                             : nullptr;
+    m.xinv[l] = c->ann_hinv[l];
+  }
   launch_ann(m, c->robot, dp, n, da, de, !(flags & IK_F_NO_LIMITS), c->d_stats, c->stream,
              c->dbg);
   IK_HIP(hipGetLastError());

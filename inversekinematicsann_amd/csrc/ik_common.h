@@ -300,7 +300,9 @@ struct AnnModelDev {
   int np[kAnnMaxLayers];  // padded out-dim (multiple of 32)
   int act[kAnnMaxLayers];
   const float4 *wp[kAnnMaxLayers];  // packed weights (see ik_ann.hip)
-  const void *wx[kAnnMaxLayers];    // bf16x6 mode: the layer's weight operand, else null
+  const void *wx[kAnnMaxLayers];    // split modes: the layer's weight operand, else null
+  float xinv[kAnnMaxLayers];        // fp16x3: 2^-k, k the layer's weight pre-scale exponent
+  int xmode;                        // 0 fp32, 1 bf16x6, 2 fp16x3 (IK_ANN_*)
   const float *bias[kAnnMaxLayers];
   double xm[3], xs[3], ym[4], ys[4];
 };
@@ -308,6 +310,9 @@ size_t ann_packed_floats(int k, int n);  // floats of one packed layer
 void ann_pack_layer(const float *W, int k, int n, float *dst);  // host-side packing
 size_t ann_x_bytes(int k, int n);  // bytes of one layer's bf16x6 weight operand
 void ann_pack_layer_x(const float *W, int k, int n, void *dst);
+size_t ann_h_bytes(int k, int n);  // bytes of one layer's fp16x3 weight operand
+int ann_h_scale_exp(const float *W, int k, int n);  // the weight pre-scale exponent k
+void ann_pack_layer_h(const float *W, int k, int n, int scale_exp, void *dst);
 size_t ann_debug_words();  // u64 slots of the diagnostic stamp buffer
 void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
                 float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,

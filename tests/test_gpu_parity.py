@@ -215,26 +215,28 @@ def test_ann_vs_oracle(ctx1, dims, act):
     assert d <= NS_TOL, d  # north_star: 1e-5 absolute
 
 
+@pytest.mark.parametrize("mode", ["bf16x6", "fp16x3"])
 @pytest.mark.parametrize("dims,act", [
     ((3,) + (500,) * 12 + (4,), "tanh"),
     ((3, 100, 37, 250, 4), "tanh"),             # ragged: K not a multiple of 16, NR 1..4
-    ((3, 512, 512, 4), "relu"),
+    ((3, 512, 512, 4), "relu"),                 # fp16x3: unbounded input -> fp32 layer
     ((3, 96, 96, 4), "sigmoid"),
 ])
-def test_ann_bf16x6_mode(ctx1, dims, act):
-    """IK_ANN_BF16X6: split-bf16 hidden GEMMs stay within the north_star 1e-5 and
-    within a small factor of the fp32 mode's own distance to a float64 forward."""
+def test_ann_split_modes(ctx1, dims, act, mode):
+    """IK_ANN_BF16X6 / IK_ANN_FP16X3: split hidden GEMMs stay within the
+    north_star 1e-5 and within a small factor of the fp32 mode's own distance to
+    a float64 forward."""
     n = 4099
     try:
-        ctx1.ann_set_mode("bf16x6")
-        assert ctx1.ann_mode() == "bf16x6"
+        ctx1.ann_set_mode(mode)
+        assert ctx1.ann_mode() == mode
         _, pts, ang_x, _, _, ref64 = _ann_case(ctx1, dims, act, n, seed=len(dims))
     finally:
         ctx1.ann_set_mode("fp32")
     ang_f, _, _ = ctx1.ann_solve(pts, check_limits=False)
     d_x = np.abs(ang_x.astype(np.float64) - ref64).max()
     d_f = np.abs(ang_f.astype(np.float64) - ref64).max()
-    print(f"bf16x6 {dims[:3]}.. {act}: max|d| {d_x:.3e} (fp32 mode {d_f:.3e})")
+    print(f"{mode} {dims[:3]}.. {act}: max|d| {d_x:.3e} (fp32 mode {d_f:.3e})")
     assert d_x <= NS_TOL, d_x             # north_star: 1e-5 absolute
     assert d_x <= 4 * d_f + 2e-7, (d_x, d_f)
 

@@ -39,7 +39,7 @@ print(json.dumps({"ms": min(ts), "ms_med": sorted(ts)[2], "max_abs_diff": d,
 
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fp32", "bf16x6"]
+    modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fp32", "bf16x6", "fp16x3"]
     for mode in modes:
       for mr in ("1", "2"):
         e = dict(os.environ, IKHIP_ANN_MR=mr, IKHIP_ANN_MODE=mode)
