@@ -103,6 +103,40 @@ __device__ __forceinline__ f32x2 act_apply2(f32x2 v) {
   }
 }
 
+// Four pairs at once, phase by phase (see layer_store).
+template <int ACT>
+__device__ __forceinline__ void act_apply2x4(f32x2 (&v)[4]) {
+  if constexpr (ACT == IK_ACT_TANH) {
+    f32x2 e[4], d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = v[k] * 2.885390081777927f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      e[k].x = __builtin_amdgcn_exp2f(-fabsf(e[k].x));
+      e[k].y = __builtin_amdgcn_exp2f(-fabsf(e[k].y));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = 1.0f + e[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = 1.0f - e[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      d[k].x = __builtin_amdgcn_rcpf(d[k].x);
+      d[k].y = __builtin_amdgcn_rcpf(d[k].y);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) e[k] = e[k] * d[k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k].x = copysignf(e[k].x, v[k].x);
+      v[k].y = copysignf(e[k].y, v[k].y);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = act_apply2<ACT>(v[k]);
+  }
+}
+
 // Operands of one 8-deep K group: A fragments of the MR 32-row tiles (LDS)
 // and the B fragments of the wave's NR column tiles (global, packed).
 template <int MR, int NR>
@@ -175,25 +209,37 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
 }
 
 // C/D map of the 32x32 MFMA: column lane & 31, row (q & 3) + 8 (q >> 2) + 4 (lane >> 5).
+// bv[j]: the bias of the lane's column in tile j, loaded before the GEMM (a
+// load issued here, after the barrier, would put a memory round trip on every
+// layer's critical path).  The activation runs on 8 elements at a time, phase
+// by phase, so the dependent exp / rcp chains of different elements overlap
+// (one element pair at a time, each step waiting on the last, cost ~100 cycles
+// per pair).
 template <int MR, int NR, int ACT>
-__device__ __forceinline__ void layer_store(float *H, const float *__restrict__ bias, int wave,
-                                            int lane, f32x16 (&acc)[MR][NR],
-                                            unsigned long long *st) {
+__device__ __forceinline__ void layer_store(float *H, const float (&bv)[NR], int wave, int lane,
+                                            f32x16 (&acc)[MR][NR], unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
   stamp(st);
   __syncthreads();  // every wave has finished reading the layer input
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int col = (wave + kWaves * j) * 32 + r;
-    const float bv = bias[col];
 #pragma unroll
     for (int m = 0; m < MR; ++m)
 #pragma unroll
-      for (int q = 0; q < 16; q += 2) {
-        const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;  // row of q + 1 is row + 1
-        const f32x2 t = act_apply2<ACT>(f32x2{acc[m][j][q], acc[m][j][q + 1]} + bv);
-        H[row * kLd + col] = t.x;
-        H[(row + 1) * kLd + col] = t.y;
+      for (int q0 = 0; q0 < 16; q0 += 8) {
+        f32x2 t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          t[k] = f32x2{acc[m][j][q0 + 2 * k], acc[m][j][q0 + 2 * k + 1]} + bv[j];
+        act_apply2x4<ACT>(t);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = q0 + 2 * k;
+          const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;  // row of q + 1 is row + 1
+          H[row * kLd + col] = t[k].x;
+          H[(row + 1) * kLd + col] = t[k].y;
+        }
       }
   }
 }
@@ -477,6 +523,9 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
                                           const void *wx = nullptr, int G16 = 0,
                                           float xinv = 1.0f) {
   f32x16 acc[MR][NR];
+  float bv[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + kWaves * j) * 32 + (lane & 31)];
   if (X == 1 && wx)
     layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, wave, lane, acc);
   else if (X == 2 && wx)
@@ -484,12 +533,10 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   else
     layer_gemm<MR, NR>(H, wp, G, 0, G, wave, kWaves, lane, acc);
   switch (act) {
-    case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bias, wave, lane, acc, st); break;
-    case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bias, wave, lane, acc, st); break;
-    case IK_ACT_SIGMOID:
-      layer_store<MR, NR, IK_ACT_SIGMOID>(H, bias, wave, lane, acc, st);
-      break;
-    default: layer_store<MR, NR, IK_ACT_LINEAR>(H, bias, wave, lane, acc, st); break;
+    case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bv, wave, lane, acc, st); break;
+    case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bv, wave, lane, acc, st); break;
+    case IK_ACT_SIGMOID: layer_store<MR, NR, IK_ACT_SIGMOID>(H, bv, wave, lane, acc, st); break;
+    default: layer_store<MR, NR, IK_ACT_LINEAR>(H, bv, wave, lane, acc, st); break;
   }
 }
 
