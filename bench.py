@@ -31,7 +31,8 @@ METRIC = "IK solutions/sec (6DOF, 1M-point batch) at 1/2/4/8 GPUs; max |FK err|"
 ANN_DIMS = (3,) + (500,) * 12 + (4,)
 FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: dense fp32 matrix peak
 BF16_MFMA_PEAK = 2.5e15     # dense bf16 matrix peak (no sparsity)
-BF16X6_PRODUCTS = 6         # bf16 MFMA products per fp32 product in the bf16x6 mode
+FP16_MFMA_PEAK = 2.5e15     # dense fp16 matrix peak (no sparsity)
+SPLIT_PRODUCTS = {"bf16x6": 6, "fp16x3": 3}  # MFMA products per fp32 product
 FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
 HBM_PEAK = 8.0e12           # bytes/s
 FABRIK_FLOP_PER_ITER = 132
@@ -50,7 +51,7 @@ def parse():
                     help="CPU-baseline time budget (rank 0, N=1); 0 disables")
     ap.add_argument("--secondary", type=int, default=1,
                     help="also time the other method and report it under 'secondary'")
-    ap.add_argument("--ann-mode", choices=["fp32", "bf16x6"], default="fp32",
+    ap.add_argument("--ann-mode", choices=["fp32", "bf16x6", "fp16x3"], default="fp32",
                     help="ANN hidden-GEMM arithmetic of the headline line (ikhip.h "
                          "ik_ann_set_mode); the other mode is reported under 'secondary'")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -168,12 +169,14 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
         lambda hp: ctx.ann_solve(hp, check_limits=True, want_fk_err=True), dpts, args, world)
     ctx.ann_set_mode("fp32")
     flop_pt = m.flops_per_point()
-    kname = "ann_fused_kernel" if mode == "fp32" else "ann_fused_kernel_bf16x6"
+    kname = "ann_fused_kernel" if mode == "fp32" else f"ann_fused_kernel_{mode}"
     k = res["kernels"].get(kname)
     achieved = flop_pt * n / (k / 1e3) if k else None
-    # bf16x6: six bf16 MFMA products per fp32 product, so the fp32-equivalent
-    # matrix peak is the bf16 peak / 6 (the input and output layers stay fp32)
-    peak = FP32_MFMA_PEAK if mode == "fp32" else BF16_MFMA_PEAK / BF16X6_PRODUCTS
+    # split modes: k bf16 / fp16 MFMA products per fp32 product, so the
+    # fp32-equivalent matrix peak is the 16-bit peak / k (the input and output
+    # layers stay fp32)
+    peak = (FP32_MFMA_PEAK if mode == "fp32" else
+            (BF16_MFMA_PEAK if mode == "bf16x6" else FP16_MFMA_PEAK) / SPLIT_PRODUCTS[mode])
     traffic = load_traffic(args.traffic_file, kname)
     res["roofline"] = {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
                        "peak": peak / 1e12, "unit": "TFLOP/s",
@@ -186,10 +189,14 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
         res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
                            f"{_pts(n)} random_dist points per GPU")
     else:
-        res["dtype"] = "fp32 via bf16x6 (3-way bf16 split, 6 MFMA products, fp32 accumulate)"
-        res["workload"] = ("ANN MLP forward (3-12x500tanh-4), hidden GEMMs in the bf16x6 mode "
-                           "(fp32-accurate: tests/test_gpu_parity.py::test_ann_bf16x6_mode) + "
-                           f"fused FK round-trip error, {_pts(n)} random_dist points per GPU")
+        res["dtype"] = {"bf16x6": "fp32 via bf16x6 (3-way bf16 split, 6 MFMA products, fp32 "
+                                  "accumulate)",
+                        "fp16x3": "fp32 via fp16x3 (2-way fp16 split of power-of-two-scaled "
+                                  "operands, 3 MFMA products, fp32 accumulate)"}[mode]
+        res["workload"] = (f"ANN MLP forward (3-12x500tanh-4), hidden GEMMs in the {mode} mode "
+                           "(accuracy: tests/test_gpu_parity.py::test_ann_split_modes and "
+                           "cpu_baseline.parity) + fused FK round-trip error, "
+                           f"{_pts(n)} random_dist points per GPU")
     return res
 
 
@@ -318,6 +325,7 @@ def cpu_baseline(method, args, sample_pts=None, gpu_out=None):
             d = float(np.abs(gpu_out["ang"][:chunk].astype(np.float64) - first).max())
             res["parity"] = {"points": chunk, "max_abs_diff_vs_oracle_fp32": d,
                              "tolerance": 1e-5, "ok": d <= 1e-5}
+        res["_ref"] = first  # for the other ANN modes' parity (dropped before printing)
         return res
     chunk = 4096
     pts = sample_pts[:chunk] if sample_pts is not None else random_dist(chunk, seed=99)
@@ -358,14 +366,16 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    other_mode = "bf16x6" if args.ann_mode == "fp32" else "fp32"
-    runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik,
-               f"ann_{other_mode}": lambda *a: run_ann(*a, mode=other_mode)}
+    other_modes = [m for m in ("fp32", "bf16x6", "fp16x3") if m != args.ann_mode]
+    runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik}
+    for om in other_modes:
+        runners[f"ann_{om}"] = (lambda mm: lambda *a: run_ann(*a, mode=mm))(om)
     res = runners[args.method](ctx, dpts, n, args, world)
     outputs = {args.method: res["outputs"]}
     secondary = {}
     if args.secondary:
-        others = ["fabrik", f"ann_{other_mode}"] if args.method == "ann" else ["ann"]
+        others = (["fabrik"] + [f"ann_{om}" for om in other_modes] if args.method == "ann"
+                  else ["ann"])
         for other in others:
             r2 = runners[other](ctx, dpts, n, args, world)
             secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
@@ -408,8 +418,21 @@ def main():
             other = "fabrik" if args.method == "ann" else "ann"
             line["secondary"][other]["cpu_baseline"] = cpu_baseline(other, args, pts,
                                                                     host(outputs[other]))
-            if other_mode == "bf16x6" and f"ann_{other_mode}" in line["secondary"]:
-                line["secondary"]["ann_bf16x6"]["cpu_baseline"] = "see top-level cpu_baseline"
+        if args.method == "ann" and args.secondary:
+            # the other ANN modes against the same oracle sample as the headline
+            ref = line["cpu_baseline"].get("_ref")
+            for om in other_modes:
+                key = f"ann_{om}"
+                if key in line["secondary"] and ref is not None:
+                    d = float(np.abs(host(outputs[key])["ang"][:ref.shape[0]]
+                                     .astype(np.float64) - ref).max())
+                    line["secondary"][key]["parity"] = {
+                        "points": int(ref.shape[0]), "max_abs_diff_vs_oracle_fp32": d,
+                        "tolerance": 1e-5, "ok": d <= 1e-5}
+        for v in [line["cpu_baseline"]] + [x.get("cpu_baseline") for x in
+                                           line.get("secondary", {}).values()]:
+            if isinstance(v, dict):
+                v.pop("_ref", None)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if _dist_on():

@@ -20,9 +20,10 @@ fi
 step bench_ann 600 python bench.py --steps ${STEPS:-10} --warmup 2 --cpu-seconds ${CPUS:-10}
 cp $OUT/bench_ann.log $OUT/bench_ann.json
 if [ "${PROFILE:-1}" = "1" ]; then
-  for m in ann fabrik ann_bf16x6; do
+  for m in ann fabrik ann_bf16x6 ann_fp16x3; do
     case $m in
       ann_bf16x6) BARGS="--method ann --ann-mode bf16x6" ;;
+      ann_fp16x3) BARGS="--method ann --ann-mode fp16x3" ;;
       *) BARGS="--method $m" ;;
     esac
     step prof_stats_$m 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_stats_$m -- python bench.py $BARGS --steps 5 --warmup 1 --cpu-seconds 0 --secondary 0

@@ -26,8 +26,10 @@ KERNELS = ("ann_fused_kernel", "fabrik_iter_kernel", "fabrik_seed_kernel",
 
 
 def _short(name: str) -> str | None:
-    if "ann_fused_kernel" in name and "true" in name:  # ann_fused_kernel<MR, true>: bf16x6 mode
-        return "ann_fused_kernel_bf16x6"
+    if "ann_fused_kernel<" in name:  # ann_fused_kernel<MR, X>: X = 0 fp32, 1 bf16x6, 2 fp16x3
+        x = name.split("ann_fused_kernel<", 1)[1].split(">", 1)[0].split(",")[-1].strip()
+        return {"1": "ann_fused_kernel_bf16x6", "2": "ann_fused_kernel_fp16x3"}.get(
+            x, "ann_fused_kernel")
     for k in KERNELS:
         if k in name:
             return k
