@@ -53,15 +53,73 @@ __device__ __forceinline__ void set_err(int &st, int code) {
 }
 
 // kinematics/point.py:32-45 get_point_between: s_c + ((d / |s-e|) * (e_c - s_c)).
-// |s-e| == 0 raises ZeroDivisionError in the reference.
+// |s-e| == 0 raises ZeroDivisionError in the reference.  The differences are
+// formed once: the distance squares s_c - e_c and fl(s_c - e_c) = -fl(e_c - s_c)
+// exactly, so squaring e_c - s_c gives the same radicand bit for bit.
 __device__ __forceinline__ d3 point_between(d3 s, d3 e, double d, int &st) {
-  double n = dist3(s, e);
+  const double dx = e.x - s.x, dy = e.y - s.y, dz = e.z - s.z;
+  double n = sqrt(sq(dx) + sq(dy) + sq(dz));
   if (n == 0.0) set_err(st, IK_E_ZERODIV);
   double q = d / n;
   d3 r;
-  r.x = s.x + (q * (e.x - s.x));
-  r.y = s.y + (q * (e.y - s.y));
-  r.z = s.z + (q * (e.z - s.z));
+  r.x = s.x + (q * dx);
+  r.y = s.y + (q * dy);
+  r.z = s.z + (q * dz);
+  return r;
+}
+
+// The compiler's correctly rounded float64 sqrt and division (the AMDGPU
+// lowerings of llvm.sqrt.f64 and fdiv double) are a Newton sequence wrapped in
+// range handling: sqrt scales radicands below 2^-767 by 2^256 and patches 0/inf
+// with v_cmp_class + selects; division pre/post-scales with v_div_scale /
+// v_div_fmas and patches specials with v_div_fixup.  Where none of that fires
+// the result is the bare sequence below, instruction for instruction, so these
+// give the same bits as sqrt() / operator/ on their domains:
+//   sqrt_core(x): 2^-767 <= x < 2^1024 (the high word of x in [hi(2^-767),
+//     hi(+inf)), which also rejects 0, negatives and NaN);
+//   div_core(a, b): b = sqrt_core(x) for such an x and 2^-100 <= |a| <= 2^100
+//   (no v_div_scale case: exponent gap < 768, quotient and 1/b normal, a not tiny).
+__device__ __forceinline__ double sqrt_core(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  h = __builtin_fma(h, r, h);
+  double e = __builtin_fma(-g, g, x);
+  g = __builtin_fma(e, h, g);
+  e = __builtin_fma(-g, g, x);
+  return __builtin_fma(e, h, g);
+}
+__device__ __forceinline__ double div_core(double a, double b) {
+  double r = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  const double q = a * r;
+  const double res = __builtin_fma(-b, q, a);
+  return __builtin_fma(res, r, q);
+}
+
+// point_between through sqrt_core / div_core.  dom accumulates the radicands'
+// distance from sqrt_core's domain (sqrt_core_dom: max over calls < kCoreDom
+// <=> all in the domain); d must be in div_core's (checked once on the host).
+// Where the domain holds the result equals point_between's and no error is
+// possible.
+constexpr uint32_t kCoreDom = 0x6FF00000u;
+__device__ __forceinline__ uint32_t sqrt_core_dom(double x) {
+  return (uint32_t)__double2hiint(x) - 0x10000000u;
+}
+__device__ __forceinline__ d3 point_between_core(d3 s, d3 e, double d, uint32_t &dom) {
+  const double dx = e.x - s.x, dy = e.y - s.y, dz = e.z - s.z;
+  const double x = sq(dx) + sq(dy) + sq(dz);
+  dom = max(dom, sqrt_core_dom(x));
+  const double q = div_core(d, sqrt_core(x));
+  d3 r;
+  r.x = s.x + (q * dx);
+  r.y = s.y + (q * dy);
+  r.z = s.z + (q * dz);
   return r;
 }
 
@@ -287,7 +345,7 @@ size_t fabrik_scratch_bytes(int64_t n);
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t st,
-                         int variant, FabOrderDev *ord);
+                         int variant, bool core, FabOrderDev *ord);
 void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,
                         const double *goals, int64_t n, double tol, int max_iter,
                         double *joints, int32_t *iters, DevStats *S, hipStream_t st);

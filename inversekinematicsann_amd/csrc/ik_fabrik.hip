@@ -38,6 +38,32 @@ __device__ __forceinline__ void fabrik_step4(const d3 start, d3 &c1, d3 &c2, d3 
   ge2 = dist3_sq(c3, g);
 }
 
+// fabrik_step4 through point_between_core: the same bits wherever dom comes back
+// below kCoreDom (then no ZeroDivisionError is possible either).  The six radicands are
+// checked against sqrt_core's domain instead of carrying the general sqrt /
+// division's range handling: ~22 % fewer instructions per iteration.
+__device__ __forceinline__ void fabrik_step4_core(const d3 start, d3 &c1, d3 &c2, d3 &c3,
+                                                  const d3 g, const double *L, double &se2,
+                                                  double &ge2, uint32_t &dom) {
+  d3 b2 = point_between_core(g, c2, L[2], dom);
+  d3 b1 = point_between_core(b2, c1, L[1], dom);
+  d3 b0 = point_between_core(b1, start, L[0], dom);
+  se2 = dist3_sq(b0, start);
+  c1 = point_between_core(start, b1, L[1], dom);
+  c2 = point_between_core(c1, b2, L[2], dom);
+  c3 = point_between_core(c2, g, L[3], dom);
+  ge2 = dist3_sq(c3, g);
+}
+
+// div_core's domain for the link lengths (the numerators): 2^-100 <= |L| <= 2^100.
+static bool links_core_ok(const double *L, int n) {
+  for (int k = 0; k < n; ++k) {
+    const double v = std::fabs(L[k]);
+    if (!(v >= 0x1p-100 && v <= 0x1p100)) return false;
+  }
+  return true;
+}
+
 // The largest x with fl(sqrt(x)) <= tol (NaN for a NaN tol, -inf for a
 // negative one), so that the reference's `sqrt(x) > tol` is `x > t` bit for
 // bit.  The loop's initial errors of 1.0 stay 1.0 (sqrt(1) = 1 exactly).
@@ -363,7 +389,7 @@ __global__ __launch_bounds__(256) void fabrik_order_scatter_kernel(FabArgs a) {
 // ORD: the queue is a.perm (work order above): a refilled lane gathers its
 // point's seed pose and goal, and writes its results at its queue position,
 // which the angles kernel maps back to the point.
-template <int REFILL_MIN, bool ORD>
+template <int REFILL_MIN, bool ORD, bool CORE>
 __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -426,7 +452,24 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
     }
     if (active) {
       if (st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step)) {
-        fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
+        if constexpr (CORE) {
+          // wave-uniform fallback: when any lane's radicand leaves sqrt_core's
+          // domain (coincident joints, non-finite input) the wave redoes the
+          // iteration with the general sqrt / division (and their errors)
+          uint32_t dom = 0;
+          d3 n1 = J1, n2 = J2, n3 = J3;
+          double se_n, ge_n;
+          fabrik_step4_core(J0, n1, n2, n3, g, L, se_n, ge_n, dom);
+          if (__all(dom < kCoreDom)) {
+            J1 = n1; J2 = n2; J3 = n3;
+            se = se_n;
+            ge = ge_n;
+          } else {
+            fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
+          }
+        } else {
+          fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
+        }
         ++step;
       } else {
         d3 J[4] = {J0, J1, J2, J3};
@@ -504,10 +547,20 @@ static int num_cus() {
   return g_cus;
 }
 
+template <int REFILL_MIN, bool ORD>
+static void launch_iter(bool core, unsigned grid, hipStream_t stream, const FabArgs &a) {
+  if (core)
+    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, true>), dim3(grid), dim3(256), 0,
+                       stream, a);
+  else
+    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, false>), dim3(grid), dim3(256), 0,
+                       stream, a);
+}
+
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
-                         int variant, FabOrderDev *ord) {
+                         int variant, bool core_req, FabOrderDev *ord) {
   if (n <= 0) return;
   FabArgs a;
   a.r = r;
@@ -595,17 +648,17 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   int64_t waves_needed = (n + 63) / 64;
   if ((int64_t)pgrid * 4 > waves_needed)
     pgrid = (unsigned)((waves_needed + 3) / 4 > 0 ? (waves_needed + 3) / 4 : 1);
+  // the iteration through sqrt_core / div_core (same bits, fewer instructions)
+  // unless the link lengths are outside div_core's domain; core_req = false
+  // (IKHIP_FABRIK_CORE=0 at context creation) forces the general sqrt / division.
+  const bool core = core_req && links_core_ok(a.r.links, 4);
   kt_begin("fabrik_iter_kernel", stream);
   if (variant == 2) {
-    if (ordered)
-      hipLaunchKernelGGL((fabrik_iter_kernel<1, true>), dim3(pgrid), dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((fabrik_iter_kernel<1, false>), dim3(pgrid), dim3(256), 0, stream, a);
+    if (ordered) launch_iter<1, true>(core, pgrid, stream, a);
+    else launch_iter<1, false>(core, pgrid, stream, a);
   } else {
-    if (ordered)
-      hipLaunchKernelGGL((fabrik_iter_kernel<8, true>), dim3(pgrid), dim3(256), 0, stream, a);
-    else
-      hipLaunchKernelGGL((fabrik_iter_kernel<8, false>), dim3(pgrid), dim3(256), 0, stream, a);
+    if (ordered) launch_iter<8, true>(core, pgrid, stream, a);
+    else launch_iter<8, false>(core, pgrid, stream, a);
   }
   kt_end(stream);
   kt_begin("fabrik_angles_kernel", stream);

@@ -323,3 +323,35 @@ def test_device_pointer_path(ctx1):
     assert np.array_equal(dit.cpu().numpy(), rit)
     assert np.abs(dang.cpu().numpy() - rang).max() <= 1e-9
     assert st.sum_iters == int(rit.sum())
+
+
+def test_fabrik_core_sequences_bit_identical():
+    """The iteration kernel's sqrt_core / div_core path (ik_common.h) claims the
+    same bits as the general sqrt / division wherever its domain check passes,
+    and falls back per wave elsewhere: final joints and iteration counts of the
+    two paths are compared bit for bit on reachable, unreachable (capped),
+    near-singular and degenerate goals."""
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    rng = np.random.default_rng(11)
+    box = rng.uniform([0.0, -6.0, -3.0], [6.0, 6.0, 6.0], size=(100_000, 3))
+    near = np.array([0.0, 0.0, 2.0]) + rng.normal(0.0, 1e-6, size=(2_000, 3))
+    near[:, 0] = np.abs(near[:, 0])
+    pts = np.concatenate([random_dist(200_000, seed=12), box, near,
+                          [[0.0, 0.0, 2.0], [1e-300, 0.0, 2.0], [0.0, 0.0, 4.0]]])
+    out = {}
+    for core in ("0", "1"):
+        os.environ["IKHIP_FABRIK_CORE"] = core
+        c = _native.Context(0)
+        os.environ.pop("IKHIP_FABRIK_CORE", None)
+        try:
+            out[core] = [c.fabrik_solve(pts, tol, mi, want_joints=True)
+                         for tol, mi in ((1e-3, 100), (1e-5, 200))]
+        finally:
+            c.close()
+    for (a0, i0, j0, s0), (a1, i1, j1, s1) in zip(out["0"], out["1"]):
+        assert np.array_equal(i0, i1)
+        assert np.array_equal(j0.view(np.uint64), j1.view(np.uint64))
+        assert np.array_equal(a0.view(np.uint64), a1.view(np.uint64))
+        assert (s0.first_oob, s0.first_err, s0.first_err_code) == \
+            (s1.first_oob, s1.first_err, s1.first_err_code)

@@ -45,6 +45,10 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "grid":  # persistent-grid size, ordered pipeline
         for bpc in ("2", "3", "4"):
             cases.append({"IKHIP_FABRIK_BPC": bpc})
+    if len(sys.argv) > 1 and sys.argv[1] == "core":  # sqrt/div core sequences on/off x grid
+        for core in ("0", "1"):
+            for bpc in ("2", "3", "4"):
+                cases.append({"IKHIP_FABRIK_CORE": core, "IKHIP_FABRIK_BPC": bpc})
     for var in (() if cases else ("1", "2", "0")):
         for bpc in ("2", "4", "8"):
             for chunk in ("64", "256"):
