@@ -85,6 +85,7 @@ struct ik_ctx {
   KTimer kt;
   unsigned long long *dbg = nullptr;  // diagnostic stamp buffer (ik_ctx_set_debug)
   FabOrderDev *fab_ord = nullptr;     // FABRIK work-order cost table (learned per robot)
+  RobotConstDev *rconst = nullptr;    // FABRIK seed-pose constants of the robot
 };
 
 namespace {
@@ -192,6 +193,7 @@ int ik_ctx_create(int device, ik_ctx **out) {
   if (e == hipSuccess) e = hipHostMalloc(&c->h_stats, sizeof(DevStats), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(&c->fab_ord, sizeof(FabOrderDev));
   if (e == hipSuccess) e = hipMemset(c->fab_ord, 0, sizeof(FabOrderDev));
+  if (e == hipSuccess) e = hipMalloc(&c->rconst, sizeof(RobotConstDev));
   if (e != hipSuccess) {
     delete c;
     return fail(IK_E_HIP, std::string("ik_ctx_create: ") + hipGetErrorString(e));
@@ -200,6 +202,13 @@ int ik_ctx_create(int device, ik_ctx **out) {
   std::memcpy(c->robot.dh, kDefaultDh, sizeof(kDefaultDh));
   std::memcpy(c->robot.links, kDefaultLinks, sizeof(kDefaultLinks));
   std::memcpy(c->robot.lim, kDefaultLimits, sizeof(kDefaultLimits));
+  launch_robot_const(c->robot, c->rconst, c->stream);
+  e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) {
+    (void)ik_ctx_destroy(c);
+    return fail(IK_E_HIP, std::string("ik_ctx_create: ") + hipGetErrorString(e));
+  }
   if (const char *v = std::getenv("IKHIP_FABRIK_VARIANT")) c->fabrik_variant = std::atoi(v);
   if (const char *v = std::getenv("IKHIP_FABRIK_CORE")) c->fabrik_core = std::atoi(v);
   if (const char *v = std::getenv("IKHIP_ANN_MODE"))
@@ -219,6 +228,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->fab_ord) (void)hipFree(c->fab_ord);
+  if (c->rconst) (void)hipFree(c->rconst);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   for (int i = 0; i < kMaxTimed; ++i) {
@@ -249,6 +259,10 @@ int ik_set_robot(ik_ctx *c, const double *dh, const double *links, const double 
     int rc = set_dev(c);
     if (rc) return rc;
     IK_HIP(hipMemsetAsync(c->fab_ord, 0, sizeof(FabOrderDev), c->stream));
+    launch_robot_const(c->robot, c->rconst, c->stream);
+    IK_HIP(hipGetLastError());
+    // synchronous: later calls may run on another stream (ik_ctx_set_stream)
+    IK_HIP(hipStreamSynchronize(c->stream));
   }
   return IK_OK;
 }
@@ -405,7 +419,7 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
   launch_reset_stats(c->d_stats, c->stream);
   launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj,
                       !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
-                      c->fabrik_variant, c->fabrik_core != 0, c->fab_ord);
+                      c->fabrik_variant, c->fabrik_core != 0, c->fab_ord, c->rconst);
   IK_HIP(hipGetLastError());
   if (!dev && n > 0) {
     IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));

@@ -217,6 +217,60 @@ __device__ __forceinline__ int fk_chain(const double *dh, const double th[4], d3
   return st;
 }
 
+// The FABRIK seed pose (inverse.py:123-130) is fk_chain at [theta_1, dh[1],
+// dh[2], dh[3]]: only theta_1 = atan2(y, x) varies per point.  A_2..A_4 at the
+// seed angles and cos/sin(alpha_1) are per-robot constants, computed once by
+// robot_const_kernel with the same device functions (hence the same bits).
+struct RobotConstDev {
+  double A[3][16];  // dh_transform(dh[k], dh[4+k], dh[8+k], dh[12+k]), k = 1..3
+  double ca1, sa1;  // cos / sin(alpha_1)
+  int st;           // fk_chain's angle check of the constant angles
+};
+
+// Rows 0-2 of C = A * B, each element the same k-ordered FMA chain as mm4.
+// Rows 0-2 of a product only read rows 0-2 of its left factor, and the chain
+// only needs the translations (rows 0-2, column 3), so row 3 is never formed.
+__device__ __forceinline__ void mm4_r3(const double *A, const double *B, double *C) {
+  double T[12];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc = fma(A[i * 4 + k], B[k * 4 + j], acc);
+      T[i * 4 + j] = acc;
+    }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) C[i] = T[i];
+}
+
+// fk_chain(dh, {th1, dh[1], dh[2], dh[3]}, J), bit for bit, from the constants:
+// A_1 = ((Rz(th1) Tz(d_1)) Tx(a_1)) Rx(alpha_1) and M_k = M_{k-1} A_k, rows 0-2.
+__device__ __forceinline__ int seed_chain(const double *dh, const RobotConstDev *rc,
+                                          double th1, d3 J[4]) {
+  double R[16], T1[16], T2[16], X[16], M[12];
+  const double c = cos(th1), s = sin(th1);
+  ident4(R);
+  R[0] = c; R[1] = -s; R[4] = s; R[5] = c;
+  ident4(T1);
+  T1[11] = dh[4];
+  ident4(T2);
+  T2[3] = dh[8];
+  ident4(X);
+  X[5] = rc->ca1; X[6] = -rc->sa1; X[9] = rc->sa1; X[10] = rc->ca1;
+  mm4_r3(R, T1, M);
+  mm4_r3(M, T2, M);
+  mm4_r3(M, X, M);
+  J[0].x = M[3]; J[0].y = M[7]; J[0].z = M[11];
+#pragma unroll
+  for (int i = 1; i < 4; ++i) {
+    mm4_r3(M, rc->A[i - 1], M);
+    J[i].x = M[3]; J[i].y = M[7]; J[i].z = M[11];
+  }
+  return rc->st;
+}
+
 // Same chain, writing all four cumulative transforms (row-major 4x4 each).
 __device__ __forceinline__ int fk_chain_mats(const double *dh, const double th[4], double *out) {
   int st = IK_OK;
@@ -345,7 +399,9 @@ size_t fabrik_scratch_bytes(int64_t n);
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t st,
-                         int variant, bool core, FabOrderDev *ord);
+                         int variant, bool core, FabOrderDev *ord, const RobotConstDev *rc);
+// Per-robot seed constants (RobotConstDev) into device memory, on stream st.
+void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t st);
 void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,
                         const double *goals, int64_t n, double tol, int max_iter,
                         double *joints, int32_t *iters, DevStats *S, hipStream_t st);

@@ -108,10 +108,30 @@ __device__ __forceinline__ void get_angles(const d3 J[4], double th[4], int &st)
 }
 
 // Seed pose, inverse.py:123-130: FK of [atan2(y, x), thetas[1:]] (the
-// reference writes theta_1 into dh_matrix[0][0] and runs fkine on that row).
-__device__ __forceinline__ int seed_pose(const RobotDev &r, d3 g, d3 J[4]) {
-  double th[4] = {atan2(g.y, g.x), r.dh[1], r.dh[2], r.dh[3]};
-  return fk_chain(r.dh, th, J);
+// reference writes theta_1 into dh_matrix[0][0] and runs fkine on that row),
+// through the per-robot constants (seed_chain; same bits as fk_chain).
+__device__ __forceinline__ int seed_pose(const RobotDev &r, const RobotConstDev *rc, d3 g,
+                                         d3 J[4]) {
+  return seed_chain(r.dh, rc, atan2(g.y, g.x), J);
+}
+
+__global__ void robot_const_kernel(RobotDev r, RobotConstDev *rc) {
+  if (threadIdx.x != 0) return;
+  int st = IK_OK;
+  for (int k = 1; k < 4; ++k) {
+    dh_transform(r.dh[k], r.dh[4 + k], r.dh[8 + k], r.dh[12 + k], rc->A[k - 1]);
+    if (!angle_ok(r.dh[k])) st = IK_E_ANGLE_RANGE;
+  }
+  for (int k = 0; k < 4; ++k)
+    if (!angle_ok(r.dh[12 + k])) st = IK_E_ANGLE_RANGE;
+  const double al = r.dh[12];
+  rc->ca1 = cos(al);
+  rc->sa1 = sin(al);
+  rc->st = st;
+}
+
+void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t stream) {
+  hipLaunchKernelGGL(robot_const_kernel, dim3(1), dim3(64), 0, stream, r, rc);
 }
 
 __device__ __forceinline__ void store_joints(double *dst, int64_t i, const d3 J[4]) {
@@ -136,6 +156,7 @@ __device__ __forceinline__ void load_joints(const double *src, int64_t i, d3 J[4
 
 struct FabArgs {
   RobotDev r;
+  const RobotConstDev *rc;  // seed constants (robot_const_kernel)
   const double *pts;
   int64_t n;
   double tol;      // fabrik.py:57 err_margin, as given
@@ -175,7 +196,7 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
     if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
       atomicMin(&a.S->first_oob, (unsigned long long)i);
     d3 J[4];
-    int st = seed_pose(a.r, g, J);
+    int st = seed_pose(a.r, a.rc, g, J);
     double se = 1.0, ge = 1.0;
     if (st == IK_OK) {
       while (((se > a.tol2) || (ge > a.tol2)) && (a.max_iter > it)) {
@@ -334,7 +355,7 @@ __global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a) {
     if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
       atomicMin(&a.S->first_oob, (unsigned long long)i);
     d3 J[4];
-    int st = seed_pose(a.r, g, J);
+    int st = seed_pose(a.r, a.rc, g, J);
     store_joints(a.seeds, i, J);
     if constexpr (ORD) {
       a.status_in[i] = (uint8_t)st;
@@ -560,10 +581,12 @@ static void launch_iter(bool core, unsigned grid, hipStream_t stream, const FabA
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
-                         int variant, bool core_req, FabOrderDev *ord) {
+                         int variant, bool core_req, FabOrderDev *ord,
+                         const RobotConstDev *rc) {
   if (n <= 0) return;
   FabArgs a;
   a.r = r;
+  a.rc = rc;
   a.pts = pts;
   a.n = n;
   a.tol = tol;
