@@ -304,6 +304,14 @@ class Context:
             raise NativeError(-n, self.lib.ik_last_error().decode())
         return out[:n].reshape(4, 4, 32) if n == out.size else out[:n]
 
+    def debug_words(self, n: int) -> np.ndarray:
+        """The first n words of the diagnostic buffer (FABRIK counters, diag build)."""
+        out = np.zeros(n, np.uint64)
+        got = self.lib.ik_debug_read(self.handle, out.ctypes.data, out.size)
+        if got < 0:
+            raise NativeError(-got, self.lib.ik_last_error().decode())
+        return out[:got]
+
     def stats_fetch(self) -> IkStats:
         s = IkStats()
         self._check(self.lib.ik_stats_fetch(self.handle, ctypes.byref(s)))

@@ -300,14 +300,19 @@ int ik_kernel_times(ik_ctx *c, int max, float *ms, char *names, int name_len) {
   return n;
 }
 
+// the diagnostic buffer: ANN stamps or FABRIK iteration-kernel counters
+static size_t debug_words() {
+  return ann_debug_words() > kFabrikDebugWords ? ann_debug_words() : kFabrikDebugWords;
+}
+
 int ik_ctx_set_debug(ik_ctx *c, int on) {
   if (!c) return fail(IK_E_BADARG, "ik_ctx_set_debug: NULL context");
   int rc = set_dev(c);
   if (rc) return rc;
   IK_HIP(hipStreamSynchronize(c->stream));
   if (on && !c->dbg) {
-    IK_HIP(hipMalloc(&c->dbg, ann_debug_words() * 8));
-    IK_HIP(hipMemset(c->dbg, 0, ann_debug_words() * 8));
+    IK_HIP(hipMalloc(&c->dbg, debug_words() * 8));
+    IK_HIP(hipMemset(c->dbg, 0, debug_words() * 8));
   } else if (!on && c->dbg) {
     IK_HIP(hipFree(c->dbg));
     c->dbg = nullptr;
@@ -319,7 +324,7 @@ int ik_debug_read(ik_ctx *c, uint64_t *out, int max) {
   if (!c || !out || max < 0) return -IK_E_BADARG;
   if (!c->dbg) return 0;
   if (set_dev(c)) return -IK_E_HIP;
-  int n = (int)ann_debug_words() < max ? (int)ann_debug_words() : max;
+  int n = (int)debug_words() < max ? (int)debug_words() : max;
   if (hipStreamSynchronize(c->stream) != hipSuccess) return -IK_E_HIP;
   if (hipMemcpy(out, c->dbg, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return -IK_E_HIP;
@@ -419,7 +424,8 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
   launch_reset_stats(c->d_stats, c->stream);
   launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj,
                       !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
-                      c->fabrik_variant, c->fabrik_core != 0, c->fab_ord, c->rconst);
+                      c->fabrik_variant, c->fabrik_core != 0, c->fab_ord, c->rconst,
+                      c->dbg);
   IK_HIP(hipGetLastError());
   if (!dev && n > 0) {
     IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));

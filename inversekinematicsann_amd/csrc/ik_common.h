@@ -375,18 +375,16 @@ void launch_check_limits(const RobotDev &r, const double *pts, int64_t n, DevSta
                          hipStream_t st);
 void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, double *mats,
                DevStats *S, hipStream_t st);
-// FABRIK work order (ik_fabrik.hip "Work order"): per context, the mean
-// iteration count of each goal cell (distance x elevation from the shoulder),
-// learned from the context's earlier calls, decides which points start first.
+// FABRIK work order (ik_fabrik.hip "Work order"): per context, the largest
+// iteration count recorded in each goal cell (distance x elevation from the
+// shoulder) on the context's earlier calls decides which points start first.
 constexpr int kOrdCellsR = 64, kOrdCellsE = 16, kOrdCells = kOrdCellsR * kOrdCellsE;
 constexpr int kOrdSample = 256;           // 1 point in 256 is recorded ...
 constexpr int kOrdMaxSample = 1 << 14;    // ... up to this many per call
 constexpr int kOrdClasses = 16;           // cost classes (queue order: hardest first)
 constexpr int kOrdMaxSeg = 2048;          // point segments of the class histogram
 struct FabOrderDev {
-  unsigned int sum[kOrdCells];  // iteration sums per cell (halved at every call)
-  unsigned int cnt[kOrdCells];  // points per cell (halved at every call)
-  float mean;                   // mean iterations over all cells (empty cells' cost)
+  unsigned int key[kOrdCells];  // 1 + largest recorded iterations per cell, 0 = unseen
   unsigned int nsample;         // (cell << 16 | iterations) records of the call
   unsigned int sample[kOrdMaxSample];
   unsigned int hist[kOrdClasses * kOrdMaxSeg];  // class counts, then scatter cursors
@@ -399,7 +397,9 @@ size_t fabrik_scratch_bytes(int64_t n);
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t st,
-                         int variant, bool core, FabOrderDev *ord, const RobotConstDev *rc);
+                         int variant, bool core, FabOrderDev *ord, const RobotConstDev *rc,
+                         unsigned long long *dbg);
+constexpr size_t kFabrikDebugWords = 64 + 4 * 4000;  // diagnostic build counters
 // Per-robot seed constants (RobotConstDev) into device memory, on stream st.
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t st);
 void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,

@@ -179,7 +179,18 @@ struct FabArgs {
   int nseg, seg_blocks;     // histogram segments, and blocks per segment
   int32_t *iters_out;       // ordered: the caller's iterations (by point), nullable
   double *joints_out;       // ordered: the caller's final joints (by point), nullable
+  unsigned long long *dbg;  // diagnostic build only: iteration-kernel counters
 };
+
+// Diagnostic counters of the iteration kernel (-DIKHIP_DIAG, libikhip_diag.so,
+// tools/fabrik_diag.py): per wave, summed into dbg[0..7], and per wave w at
+// dbg[64 + 4w ..]: s_memrealtime (100 MHz) at start, when the queue ran dry
+// for it and at the end, and the steps it ran after the queue ran dry.
+enum { kDiagLoops, kDiagSteps, kDiagLaneSteps, kDiagRefills, kDiagGrabs, kDiagFallbacks,
+       kDiagWaves, kDiagCount };
+#ifdef IKHIP_DIAG
+constexpr int kDiagWaveMax = 4000;  // = (kFabrikDebugWords - 64) / 4
+#endif
 
 static int env_int(const char *name, int dflt) {
   const char *v = getenv(name);
@@ -228,12 +239,17 @@ __global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a);
 // order a 100-iteration point can be picked up just before the queue runs dry
 // and set the launch length alone (≈ 1.4x the lane-iterations / lanes bound
 // at 1M random_dist points).  Handing out the expensive points first removes
-// most of that tail (a list-scheduling simulation of the kernel's refill rule
-// on reference iteration counts: 1.44x -> 1.09x the bound).  The cost of a
-// point is predicted from its goal cell -- distance from the shoulder (the
-// first joint) in 64 bins up to the reach of links 1..3, and the sine of the
-// elevation in 16 bins -- by the mean iteration count the context recorded in
-// that cell on earlier calls (1 point in kOrdSample, halved at each call).
+// most of that tail.  The cost of a point is predicted from its goal cell --
+// distance from the shoulder (the first joint) in 64 bins up to the reach of
+// links 1..3, and the sine of the elevation in 16 bins -- by the LARGEST
+// iteration count the context recorded in that cell on earlier calls (1 point
+// in kOrdSample; the old key decays by 1/8 when new records arrive).  The
+// largest, not the mean: what sets the tail is a long point starting late, and
+// long points (9 % of random_dist points take >= 80 of 100 iterations) sit in
+// cells of every mean.  A list-scheduling simulation of 131k lanes on 1M
+// reference iteration counts (tol 1e-3 / 1e-5): point order 1.29x / 1.34x the
+// lane-iterations / lanes bound, cells by mean 1.15x / 1.23x, cells by sampled
+// max 1.04x / 1.03x, exact longest-first 1.01x.  Unseen cells count as hard.
 // Costs map to 16 classes; a counting sort (class-major, hardest first; order
 // inside a class is whatever the atomics give) yields the queue -> point
 // permutation.  Results do not depend on the order: every point is still
@@ -258,9 +274,9 @@ __device__ __forceinline__ int goal_cell(const RobotDev &r, d3 g, d3 shoulder) {
 }
 
 __device__ __forceinline__ int cost_class(const FabOrderDev *T, int cell, int max_iter) {
-  const unsigned int n = T->cnt[cell];
-  const float mean = n ? (float)T->sum[cell] / (float)n : T->mean;
-  const int k = (int)(mean * kOrdClasses / (float)(max_iter + 1));
+  const unsigned int key = T->key[cell];  // 1 + largest recorded iterations, 0 = unseen
+  if (key == 0) return kOrdClasses - 1;
+  const int k = (int)((long long)(key - 1) * kOrdClasses / (max_iter + 1));
   return k < 0 ? 0 : (k >= kOrdClasses ? kOrdClasses - 1 : k);
 }
 
@@ -293,43 +309,27 @@ __device__ void order_scan(FabOrderDev *T, int nseg) {
   }
 }
 
-// Fold the records into the halved table and refresh the mean.  One block.
+// Fold the records into the table: per cell, the largest recorded iteration
+// count of the call, or the decayed old key if larger.  One block.
 __device__ void order_fold(FabOrderDev *T) {
-  __shared__ unsigned int ls[kOrdCells], lc[kOrdCells];
-  __shared__ unsigned long long red[2][4];
+  __shared__ unsigned int lm[kOrdCells];
   const int t = threadIdx.x;
-  for (int c = t; c < kOrdCells; c += 256) {
-    ls[c] = T->sum[c] >> 1;
-    lc[c] = T->cnt[c] >> 1;
-  }
+  for (int c = t; c < kOrdCells; c += 256) lm[c] = 0;
   __syncthreads();
   const unsigned int ns = T->nsample < kOrdMaxSample ? T->nsample : kOrdMaxSample;
   for (unsigned int k = t; k < ns; k += 256) {
     const unsigned int v = T->sample[k];
-    atomicAdd(&ls[v >> 16], v & 0xffffu);
-    atomicAdd(&lc[v >> 16], 1u);
+    atomicMax(&lm[v >> 16], (v & 0xffffu) + 1u);
   }
   __syncthreads();
-  unsigned long long s = 0, n = 0;
   for (int c = t; c < kOrdCells; c += 256) {
-    T->sum[c] = ls[c];
-    T->cnt[c] = lc[c];
-    s += ls[c];
-    n += lc[c];
+    if (lm[c]) {
+      const unsigned int old = T->key[c];
+      const unsigned int dec = old - (old >> 3);
+      T->key[c] = lm[c] > dec ? lm[c] : dec;
+    }
   }
-  s = wave_sum_u64(s);
-  n = wave_sum_u64(n);
-  if ((t & 63) == 0) {
-    red[0][t >> 6] = s;
-    red[1][t >> 6] = n;
-  }
-  __syncthreads();
-  if (t == 0) {
-    const unsigned long long ts = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    const unsigned long long tc = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    T->mean = tc ? (float)((double)ts / (double)tc) : 0.0f;
-    T->nsample = 0;
-  }
+  if (t == 0) T->nsample = 0;
 }
 
 // One block: this call's class counts -> cursors, then the previous call's
@@ -426,16 +426,27 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   double se = 1.0, ge = 1.0;
   int step = 0, st = IK_OK;
 
+#ifdef IKHIP_DIAG
+  unsigned long long dg[kDiagCount] = {};
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+  unsigned long long t_dry = 0, steps_dry = 0;
+#define IKHIP_DG(k, v) (dg[k] += (v))
+#else
+#define IKHIP_DG(k, v) ((void)0)
+#endif
   while (true) {
     unsigned long long freem = __ballot(!active);
     int nfree = __popcll(freem);
     if (exhausted && nfree == 64) break;
+    IKHIP_DG(kDiagLoops, 1);
     if (!exhausted && (nfree >= REFILL_MIN || nfree == 64)) {
+      IKHIP_DG(kDiagRefills, 1);
       int rank = __popcll(freem & lt_mask);
       int64_t mine = -1;
       int handed = 0;
       while (handed < nfree) {
         if (qnext >= qend) {
+          IKHIP_DG(kDiagGrabs, 1);
           unsigned long long old = 0;
           if (lane == 0) old = atomicAdd(&a.S->queue, (unsigned long long)a.chunk);
           old = __shfl(old, 0, 64);
@@ -471,6 +482,18 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
         active = true;
       }
     }
+#ifdef IKHIP_DIAG
+    {
+      const unsigned long long sm =
+          __ballot(active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step));
+      dg[kDiagSteps] += sm ? 1 : 0;
+      dg[kDiagLaneSteps] += __popcll(sm);
+      if (exhausted) {
+        if (!t_dry) t_dry = __builtin_amdgcn_s_memrealtime();
+        steps_dry += sm ? 1 : 0;
+      }
+    }
+#endif
     if (active) {
       if (st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step)) {
         if constexpr (CORE) {
@@ -486,6 +509,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
             se = se_n;
             ge = ge_n;
           } else {
+            IKHIP_DG(kDiagFallbacks, 1);
             fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
           }
         } else {
@@ -501,6 +525,20 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
       }
     }
   }
+#ifdef IKHIP_DIAG
+  if (a.dbg && lane == 0) {
+    dg[kDiagWaves] = 1;
+    for (int k = 0; k < kDiagCount; ++k) atomicAdd(&a.dbg[k], dg[k]);
+    const int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+    if (w < kDiagWaveMax) {
+      a.dbg[64 + 4 * w] = t_start;
+      a.dbg[65 + 4 * w] = t_dry;
+      a.dbg[66 + 4 * w] = __builtin_amdgcn_s_memrealtime();
+      a.dbg[67 + 4 * w] = steps_dry;
+    }
+  }
+#endif
+#undef IKHIP_DG
 }
 
 // 3. angles + stats (uniform work, one point per lane).  ORD: the iteration
@@ -582,11 +620,12 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
                          int variant, bool core_req, FabOrderDev *ord,
-                         const RobotConstDev *rc) {
+                         const RobotConstDev *rc, unsigned long long *dbg) {
   if (n <= 0) return;
   FabArgs a;
   a.r = r;
   a.rc = rc;
+  a.dbg = dbg;
   a.pts = pts;
   a.n = n;
   a.tol = tol;
@@ -675,6 +714,9 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   // unless the link lengths are outside div_core's domain; core_req = false
   // (IKHIP_FABRIK_CORE=0 at context creation) forces the general sqrt / division.
   const bool core = core_req && links_core_ok(a.r.links, 4);
+#ifdef IKHIP_DIAG
+  if (a.dbg) (void)hipMemsetAsync(a.dbg, 0, kFabrikDebugWords * 8, stream);
+#endif
   kt_begin("fabrik_iter_kernel", stream);
   if (variant == 2) {
     if (ordered) launch_iter<1, true>(core, pgrid, stream, a);

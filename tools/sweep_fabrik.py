@@ -56,7 +56,8 @@ if __name__ == "__main__":
                     continue
                 cases.append({"IKHIP_FABRIK_VARIANT": var, "IKHIP_FABRIK_BPC": bpc,
                               "IKHIP_FABRIK_CHUNK": chunk})
-    for n, tol, mi in ((1_000_000, 1e-3, 100), (1_000_000, 1e-5, 200)):
+    n_pts = int(os.environ.get("SWEEP_N", "1000000"))
+    for n, tol, mi in ((n_pts, 1e-3, 100), (n_pts, 1e-5, 200)):
         for c in cases:
             r = run(c, n, tol, mi)
             tot = sum(v for v in r.values() if isinstance(v, float))
