@@ -40,11 +40,14 @@ print(json.dumps({"ms": min(ts), "ms_med": sorted(ts)[2], "max_abs_diff": d,
 if __name__ == "__main__":
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
     modes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fp32", "bf16x6", "fp16x3"]
+    mrs = os.environ.get("SWEEP_MR", "1,2").split(",")
+    extra = [kv.split("=", 1) for kv in os.environ.get("SWEEP_ENV", "").split(";") if kv]
     for mode in modes:
-      for mr in ("1", "2"):
-        e = dict(os.environ, IKHIP_ANN_MR=mr, IKHIP_ANN_MODE=mode)
+     for env in ([{}] + [{k: v} for k, v in extra]):
+      for mr in mrs:
+        e = dict(os.environ, IKHIP_ANN_MR=mr, IKHIP_ANN_MODE=mode, **env)
         out = subprocess.run([sys.executable, "-c", CODE, str(n)], env=e, capture_output=True,
                              text=True, timeout=600)
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
-        print(json.dumps({"MR": mr, "mode": mode, **(json.loads(line[-1]) if line else
+        print(json.dumps({"MR": mr, "mode": mode, **env, **(json.loads(line[-1]) if line else
                                        {"error": out.stderr[-800:]})}), flush=True)
