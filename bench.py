@@ -200,8 +200,10 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
     return res
 
 
-def run_fabrik(ctx, dpts, n, args, world):
+def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
     import torch
+    tol = args.tol if tol is None else tol
+    max_iter = args.max_iter if max_iter is None else max_iter
     from inversekinematicsann_amd import _native
     dang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
     dit = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -210,7 +212,7 @@ def run_fabrik(ctx, dpts, n, args, world):
     gather = make_gather(dang, args, world)
 
     def step():
-        ctx.fabrik_solve_device(dpts, dang, dit, None, args.tol, args.max_iter, flags=flags)
+        ctx.fabrik_solve_device(dpts, dang, dit, None, tol, max_iter, flags=flags)
         gather()
 
     res = timed(ctx, step, args, world)
@@ -219,7 +221,7 @@ def run_fabrik(ctx, dpts, n, args, world):
     res["n_capped"] = st.n_capped
     res["outputs"] = {"ang": dang, "iters": dit}
     res["end_to_end"] = end_to_end(
-        lambda hp: ctx.fabrik_solve(hp, args.tol, args.max_iter), dpts, args, world)
+        lambda hp: ctx.fabrik_solve(hp, tol, max_iter), dpts, args, world)
     k = res["kernels"].get("fabrik_iter_kernel")
     flops = FABRIK_FLOP_PER_ITER * st.sum_iters
     achieved = flops / (k / 1e3) if k else None
@@ -231,8 +233,8 @@ def run_fabrik(ctx, dpts, n, args, world):
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
                        "iterations_per_launch": int(st.sum_iters)}
     res["dtype"] = "f64"
-    res["workload"] = (f"FABRIK ikine (seed FK + loop + angles), tol {args.tol:g} / "
-                       f"{args.max_iter} iterations, float64, {_pts(n)} random_dist points per GPU")
+    res["workload"] = (f"FABRIK ikine (seed FK + loop + angles), tol {tol:g} / "
+                       f"{max_iter} iterations, float64, {_pts(n)} random_dist points per GPU")
     return res
 
 
@@ -367,15 +369,19 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     other_modes = [m for m in ("fp32", "bf16x6", "fp16x3") if m != args.ann_mode]
-    runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik}
+    runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik,
+               # configs[4]'s divergent-iteration stress settings on the per-GPU batch
+               "fabrik_tol1e-5": lambda *a: run_fabrik(*a, tol=1e-5, max_iter=200)}
     for om in other_modes:
         runners[f"ann_{om}"] = (lambda mm: lambda *a: run_ann(*a, mode=mm))(om)
     res = runners[args.method](ctx, dpts, n, args, world)
     outputs = {args.method: res["outputs"]}
     secondary = {}
     if args.secondary:
-        others = (["fabrik"] + [f"ann_{om}" for om in other_modes] if args.method == "ann"
-                  else ["ann"])
+        others = (["fabrik", "fabrik_tol1e-5"] + [f"ann_{om}" for om in other_modes]
+                  if args.method == "ann" else ["ann", "fabrik_tol1e-5"])
+        if args.method == "fabrik" and (args.tol, args.max_iter) == (1e-5, 200):
+            others.remove("fabrik_tol1e-5")
         for other in others:
             r2 = runners[other](ctx, dpts, n, args, world)
             secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
