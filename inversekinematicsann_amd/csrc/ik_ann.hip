@@ -32,6 +32,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kLd = 516;   // LDS row stride in floats (>= 512 + 4)
 constexpr int kWaves = 4;  // waves per workgroup
+constexpr int kHPad = 64;  // floats past the last activation row (see layer_gemm)
 
 struct AnnArgs {
   AnnModelDev m;
@@ -148,10 +149,25 @@ struct Frag {
 template <int MR, int NR>
 __device__ __forceinline__ void load_group(Frag<MR, NR> &f, const float *ap,
                                            const f32x4 *const (&bp)[NR], int g) {
+#ifdef IKHIP_DIAG_NOLOAD
+  if (g > 2) return;  // timing experiment: the ring keeps its first operands
+#endif
+  // IKHIP_DIAG_WSAME / _ASAME (timing experiments only, wrong results): every
+  // group reads the weights / activations of group 0 (L1-resident / same LDS line)
+#ifdef IKHIP_DIAG_ASAME
+  const int ga = 0;
+#else
+  const int ga = g;
+#endif
+#ifdef IKHIP_DIAG_WSAME
+  const int gb = g & 1;
+#else
+  const int gb = g;
+#endif
 #pragma unroll
-  for (int m = 0; m < MR; ++m) f.a[m] = *reinterpret_cast<const f32x4 *>(ap + m * 32 * kLd + 8 * g);
+  for (int m = 0; m < MR; ++m) f.a[m] = *reinterpret_cast<const f32x4 *>(ap + m * 32 * kLd + 8 * ga);
 #pragma unroll
-  for (int j = 0; j < NR; ++j) f.b[j] = bp[j][(size_t)g * 64];
+  for (int j = 0; j < NR; ++j) f.b[j] = bp[j][(size_t)gb * 64];
 }
 
 template <int MR, int NR>
@@ -179,23 +195,76 @@ __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[M
 #define IKHIP_ANN_RING 4
 #endif
 constexpr int kRing = IKHIP_ANN_RING;
+#ifndef IKHIP_ANN_BUF
+#define IKHIP_ANN_BUF 1
+#endif
 
 template <int MR, int NR>
 __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restrict__ wp, int G,
-                                           int g0, int g1, int nt0, int nt_stride, int lane,
-                                           f32x16 (&acc)[MR][NR]) {
+                                           int wbytes, int g0, int g1, int nt0, int nt_stride,
+                                           int lane, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 4 * h;
-  const f32x4 *bp[NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    bp[j] = wp + (size_t)(nt0 + nt_stride * j) * G * 64 + lane;
+  for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
-  }
   if (g1 <= g0) return;
-  const int last = g1 - 1;
   Frag<MR, NR> f[kRing];
+#if IKHIP_ANN_BUF
+  // The weight stream through a buffer descriptor over the layer (wave-uniform
+  // base and size): each load is one buffer_load_dwordx4 with the lane's tile
+  // offset in a VGPR fixed for the layer, the group in an SGPR and the ring
+  // slot in the immediate offset -- no per-load 64-bit address arithmetic.
+  // Groups past the layer's end read zeros (range check); groups past a
+  // tile's K range read the next tile's data, which is never multiplied.
+  const uint64_t wpi = reinterpret_cast<uint64_t>(wp);
+  const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wpi);
+  const uint32_t whi = __builtin_amdgcn_readfirstlane((uint32_t)(wpi >> 32));
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(((uint64_t)whi << 32) | wlo), 0,
+      __builtin_amdgcn_readfirstlane(wbytes), 0x00020000);
+  int vo[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) vo[j] = ((nt0 + nt_stride * j) * G * 64 + lane) * 16;
+  auto load_b = [&](Frag<MR, NR> &fr, int gbase, int u) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+      fr.b[j] = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo[j], (gbase + u) * 1024, 0));
+  };
+  // A fragments: one base address per ring pass, the slot in the ds_read
+  // immediate offset.  Reads run up to kRing - 1 groups past the K range
+  // (into the next row, or the pad at the end of H), never multiplied.
+  auto load_a = [&](Frag<MR, NR> &fr, const float *a0, int u) {
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+      fr.a[m] = *reinterpret_cast<const f32x4 *>(a0 + m * 32 * kLd + 8 * u);
+  };
+#pragma unroll
+  for (int u = 0; u < kRing - 1; ++u) {  // group by group, as the loop issues them
+    load_a(f[u], ap + 8 * g0, u);
+    load_b(f[u], g0, u);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  int g = g0;
+  for (; g + kRing <= g1; g += kRing) {
+    const float *a0 = ap + 8 * (g + kRing - 1);
+#pragma unroll
+    for (int u = 0; u < kRing; ++u) {
+      load_a(f[(u + kRing - 1) % kRing], a0, u);
+      load_b(f[(u + kRing - 1) % kRing], g + kRing - 1, u);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_group(f[u], acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#else
+  (void)wbytes;
+  const int last = g1 - 1;
+  const f32x4 *bp[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) bp[j] = wp + (size_t)(nt0 + nt_stride * j) * G * 64 + lane;
 #pragma unroll
   for (int u = 0; u < kRing - 1; ++u) load_group(f[u], ap, bp, min(g0 + u, last));
   int g = g0;
@@ -208,6 +277,7 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+#endif
 #pragma unroll
   for (int u = 0; u < kRing - 1; ++u)
     if (g + u < g1) mma_group(f[u], acc);
@@ -524,7 +594,7 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
 // a layer that stays fp32.
 template <int MR, int NR, int X = 0>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
-                                          int G, int wave, int lane, unsigned long long *st,
+                                          int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           const void *wx = nullptr, int G16 = 0,
                                           float xinv = 1.0f) {
   f32x16 acc[MR][NR];
@@ -536,7 +606,7 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   else if (X == 2 && wx)
     layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, xinv, wave, lane, acc);
   else
-    layer_gemm<MR, NR>(H, wp, G, 0, G, wave, kWaves, lane, acc);
+    layer_gemm<MR, NR>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, acc);
   switch (act) {
     case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bv, wave, lane, acc, st); break;
     case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bv, wave, lane, acc, st); break;
@@ -566,7 +636,7 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
   constexpr int BM = 32 * MR;
   f32x16 acc[MR][1];
   const int g0 = (G * wave) / kWaves, g1 = (G * (wave + 1)) / kWaves;
-  layer_gemm<MR, 1>(H, wp, G, g0, g1, 0, 0, lane, acc);
+  layer_gemm<MR, 1>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, acc);
   stamp(st);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
@@ -621,7 +691,8 @@ __device__ __forceinline__ double fk_error(const double *jc, const double th[4],
 template <int MR, int X>
 __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnArgs a) {
   constexpr int BM = 32 * MR;
-  __shared__ __attribute__((aligned(16))) float H[BM * kLd];
+  // + kHPad: the fp32 GEMM's operand ring reads up to 3 K groups past a row's end
+  __shared__ __attribute__((aligned(16))) float H[BM * kLd + kHPad];
   const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63;
   const int64_t ntiles = (a.n + BM - 1) / BM;
@@ -672,19 +743,19 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
         const int G16 = (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
-          case 3: run_layer<MR, 3, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
-          case 2: run_layer<MR, 2, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
-          case 1: run_layer<MR, 1, X>(H, wp, bias, act, G, wave, lane, sl, wx, G16, xinv); break;
+          case 4: run_layer<MR, 4, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
+          case 3: run_layer<MR, 3, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
+          case 2: run_layer<MR, 2, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
+          case 1: run_layer<MR, 1, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
           default: __syncthreads(); break;
         }
       } else {
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4>(H, wp, bias, act, G, wave, lane, sl); break;
-          case 3: run_layer<MR, 3>(H, wp, bias, act, G, wave, lane, sl); break;
-          case 2: run_layer<MR, 2>(H, wp, bias, act, G, wave, lane, sl); break;
-          case 1: run_layer<MR, 1>(H, wp, bias, act, G, wave, lane, sl); break;
+          case 4: run_layer<MR, 4>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
+          case 3: run_layer<MR, 3>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
+          case 2: run_layer<MR, 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
+          case 1: run_layer<MR, 1>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
           default: __syncthreads(); break;  // idle wave still joins the barrier
         }
       }
