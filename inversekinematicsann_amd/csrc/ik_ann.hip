@@ -170,6 +170,39 @@ __device__ __forceinline__ void load_group(Frag<MR, NR> &f, const float *ap,
   for (int j = 0; j < NR; ++j) f.b[j] = bp[j][(size_t)gb * 64];
 }
 
+// A wave's weight stream over one layer operand through a buffer descriptor
+// (wave-uniform base and size): each load is one buffer_load_dwordx4 with the
+// lane's column-tile offset in a VGPR fixed for the layer and the 1 KiB block
+// index in soffset -- no per-load 64-bit address arithmetic, whose issue cost
+// beside the MFMAs is what the loop overhead mostly was (DESIGN.md "ANN").
+// Blocks past the operand's end read zeros (range check), so prefetches need
+// no clamp; blocks past a tile's K range read the next tile, never multiplied.
+template <int NR>
+struct WStream {
+  __amdgpu_buffer_rsrc_t rs;
+  int vo[NR];
+};
+
+template <int NR>
+__device__ __forceinline__ WStream<NR> make_wstream(const void *base, int bytes, int nt0,
+                                                    int nt_stride, int blocks_per_tile,
+                                                    int lane) {
+  WStream<NR> w;
+  const uint64_t bi = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bi);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bi >> 32));
+  w.rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(((uint64_t)hi << 32) | lo),
+                                           0, __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < NR; ++j) w.vo[j] = ((nt0 + nt_stride * j) * blocks_per_tile * 64 + lane) * 16;
+  return w;
+}
+
+template <typename T, int NR>
+__device__ __forceinline__ T wload(const WStream<NR> &w, int j, int blk) {
+  return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.vo[j], blk * 1024, 0));
+}
+
 template <int MR, int NR>
 __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[MR][NR]) {
 #pragma unroll
@@ -218,20 +251,10 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
   // slot in the immediate offset -- no per-load 64-bit address arithmetic.
   // Groups past the layer's end read zeros (range check); groups past a
   // tile's K range read the next tile's data, which is never multiplied.
-  const uint64_t wpi = reinterpret_cast<uint64_t>(wp);
-  const uint32_t wlo = __builtin_amdgcn_readfirstlane((uint32_t)wpi);
-  const uint32_t whi = __builtin_amdgcn_readfirstlane((uint32_t)(wpi >> 32));
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void *>(((uint64_t)whi << 32) | wlo), 0,
-      __builtin_amdgcn_readfirstlane(wbytes), 0x00020000);
-  int vo[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) vo[j] = ((nt0 + nt_stride * j) * G * 64 + lane) * 16;
+  const WStream<NR> ws = make_wstream<NR>(wp, wbytes, nt0, nt_stride, G, lane);
   auto load_b = [&](Frag<MR, NR> &fr, int gbase, int u) {
 #pragma unroll
-    for (int j = 0; j < NR; ++j)
-      fr.b[j] = __builtin_bit_cast(
-          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo[j], (gbase + u) * 1024, 0));
+    for (int j = 0; j < NR; ++j) fr.b[j] = wload<f32x4>(ws, j, gbase + u);
   };
   // A fragments: one base address per ring pass, the slot in the ds_read
   // immediate offset.  Reads run up to kRing - 1 groups past the K range
@@ -370,11 +393,11 @@ struct WStep {
 };
 
 template <int NR>
-__device__ __forceinline__ void load_w(WStep<NR> &w, const bf16x8 *const (&bp)[NR], int g) {
+__device__ __forceinline__ void load_w(WStep<NR> &w, const WStream<NR> &ws, int g) {
 #pragma unroll
   for (int j = 0; j < NR; ++j)
 #pragma unroll
-    for (int p = 0; p < 3; ++p) w.p[j][p] = bp[j][((size_t)g * 3 + p) * 64];
+    for (int p = 0; p < 3; ++p) w.p[j][p] = wload<bf16x8>(ws, j, g * 3 + p);
 }
 
 // A fragments of K step g (lane: row lane&31, k 16g + 8*(lane>>5) + 0..7), two ds_read_b128.
@@ -393,14 +416,14 @@ __device__ __forceinline__ void load_a(f32x8 (&a)[MR], const float *ap, int g) {
 // g+2 (into the buffer step g-1 used: three buffers in flight, two steps of
 // L2 latency covered) and A of step g+1, read from LDS and split in VALU
 // between the MFMAs (sched_group_barrier pattern below), into sa for the next step.
-template <int MR, int NR>
+template <int MR, int NR, int GI>
 __device__ __forceinline__ void step_x(Split3 (&sa)[MR], const WStep<NR> &w, WStep<NR> &fill,
-                                       const bf16x8 *const (&bp)[NR], const float *ap, int g,
-                                       int last, f32x16 (&acc)[MR][NR]) {
+                                       const WStream<NR> &ws, const float *ab, int g,
+                                       f32x16 (&acc)[MR][NR]) {
   __builtin_amdgcn_sched_barrier(0);
-  load_w(fill, bp, min(g + 2, last));
+  load_w(fill, ws, g + 2);
   f32x8 an[MR];
-  load_a(an, ap, min(g + 1, last));
+  load_a(an, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
   Split3 sn[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) sn[m] = split3(an[m]);
@@ -432,23 +455,22 @@ __device__ __forceinline__ void step_x(Split3 (&sa)[MR], const WStep<NR> &w, WSt
   for (int m = 0; m < MR; ++m) sa[m] = sn[m];
 }
 
-// Full-width layer in bf16x6 mode (NR column tiles per wave).
+// Full-width layer in bf16x6 mode (NR column tiles per wave).  A reads of the
+// step after the last run into the next row or H's pad, never multiplied.
 template <int MR, int NR>
 __device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__restrict__ wx,
-                                             int G16, int wave, int lane, f32x16 (&acc)[MR][NR]) {
+                                             int G16, int xbytes, int wave, int lane,
+                                             f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 8 * h;
-  const bf16x8 *bp[NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    bp[j] = wx + (size_t)(wave + kWaves * j) * G16 * 3 * 64 + lane;
+  for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
-  }
-  const int last = G16 - 1;
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 3, lane);
   WStep<NR> w0, w1, w2;
-  load_w(w0, bp, 0);
-  load_w(w1, bp, min(1, last));
+  load_w(w0, ws, 0);
+  load_w(w1, ws, 1);
   Split3 sa[MR];
   {
     f32x8 a0[MR];
@@ -458,12 +480,14 @@ __device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__res
   }
   int g = 0;
   for (; g + 3 <= G16; g += 3) {
-    step_x<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
-    step_x<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
-    step_x<MR, NR>(sa, w2, w1, bp, ap, g + 2, last, acc);
+    const float *ab = ap + 16 * g;
+    step_x<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
+    step_x<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
+    step_x<MR, NR, 2>(sa, w2, w1, ws, ab, g + 2, acc);
   }
-  if (g < G16) step_x<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
-  if (g + 1 < G16) step_x<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
+  const float *ab = ap + 16 * g;
+  if (g < G16) step_x<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
+  if (g + 1 < G16) step_x<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
 }
 
 // ------------------------------------------------- split-fp16 (fp16x3) mode ----
@@ -507,23 +531,23 @@ struct WStepH {
 };
 
 template <int NR>
-__device__ __forceinline__ void load_wh(WStepH<NR> &w, const f16x8 *const (&bp)[NR], int g) {
+__device__ __forceinline__ void load_wh(WStepH<NR> &w, const WStream<NR> &ws, int g) {
 #pragma unroll
   for (int j = 0; j < NR; ++j)
 #pragma unroll
-    for (int p = 0; p < 2; ++p) w.p[j][p] = bp[j][((size_t)g * 2 + p) * 64];
+    for (int p = 0; p < 2; ++p) w.p[j][p] = wload<f16x8>(ws, j, g * 2 + p);
 }
 
 // One K step (see step_x): weights of step g+2 and A of step g+1 in the shadow
 // of the 3 * MR * NR MFMAs of step g.
-template <int MR, int NR>
+template <int MR, int NR, int GI>
 __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WStepH<NR> &fill,
-                                       const f16x8 *const (&bp)[NR], const float *ap, int g,
-                                       int last, f32x16 (&acc)[MR][NR]) {
+                                       const WStream<NR> &ws, const float *ab, int g,
+                                       f32x16 (&acc)[MR][NR]) {
   __builtin_amdgcn_sched_barrier(0);
-  load_wh(fill, bp, min(g + 2, last));
+  load_wh(fill, ws, g + 2);
   f32x8 an[MR];
-  load_a(an, ap, min(g + 1, last));
+  load_a(an, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
   Split2 sn[MR];
 #pragma unroll
   for (int m = 0; m < MR; ++m) sn[m] = split2h(an[m]);
@@ -553,21 +577,18 @@ __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WS
 // Full-width layer in fp16x3 mode; the accumulators come back scaled by xinv.
 template <int MR, int NR>
 __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__restrict__ wx,
-                                             int G16, float xinv, int wave, int lane,
+                                             int G16, int xbytes, float xinv, int wave, int lane,
                                              f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 8 * h;
-  const f16x8 *bp[NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    bp[j] = wx + (size_t)(wave + kWaves * j) * G16 * 2 * 64 + lane;
+  for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
-  }
-  const int last = G16 - 1;
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 2, lane);
   WStepH<NR> w0, w1, w2;
-  load_wh(w0, bp, 0);
-  load_wh(w1, bp, min(1, last));
+  load_wh(w0, ws, 0);
+  load_wh(w1, ws, 1);
   Split2 sa[MR];
   {
     f32x8 a0[MR];
@@ -577,12 +598,14 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
   }
   int g = 0;
   for (; g + 3 <= G16; g += 3) {
-    step_h<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
-    step_h<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
-    step_h<MR, NR>(sa, w2, w1, bp, ap, g + 2, last, acc);
+    const float *ab = ap + 16 * g;
+    step_h<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
+    step_h<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
+    step_h<MR, NR, 2>(sa, w2, w1, ws, ab, g + 2, acc);
   }
-  if (g < G16) step_h<MR, NR>(sa, w0, w2, bp, ap, g, last, acc);
-  if (g + 1 < G16) step_h<MR, NR>(sa, w1, w0, bp, ap, g + 1, last, acc);
+  const float *ab = ap + 16 * g;
+  if (g < G16) step_h<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
+  if (g + 1 < G16) step_h<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
 #pragma unroll
   for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -601,10 +624,13 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   float bv[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + kWaves * j) * 32 + (lane & 31)];
+  const int NT = wbytes / (G * 1024);  // column tiles of the layer
   if (X == 1 && wx)
-    layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, wave, lane, acc);
+    layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024, wave,
+                         lane, acc);
   else if (X == 2 && wx)
-    layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, xinv, wave, lane, acc);
+    layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024, xinv,
+                         wave, lane, acc);
   else
     layer_gemm<MR, NR>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, acc);
   switch (act) {
