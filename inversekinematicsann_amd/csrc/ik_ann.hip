@@ -146,30 +146,6 @@ struct Frag {
   f32x4 b[NR];
 };
 
-template <int MR, int NR>
-__device__ __forceinline__ void load_group(Frag<MR, NR> &f, const float *ap,
-                                           const f32x4 *const (&bp)[NR], int g) {
-#ifdef IKHIP_DIAG_NOLOAD
-  if (g > 2) return;  // timing experiment: the ring keeps its first operands
-#endif
-  // IKHIP_DIAG_WSAME / _ASAME (timing experiments only, wrong results): every
-  // group reads the weights / activations of group 0 (L1-resident / same LDS line)
-#ifdef IKHIP_DIAG_ASAME
-  const int ga = 0;
-#else
-  const int ga = g;
-#endif
-#ifdef IKHIP_DIAG_WSAME
-  const int gb = g & 1;
-#else
-  const int gb = g;
-#endif
-#pragma unroll
-  for (int m = 0; m < MR; ++m) f.a[m] = *reinterpret_cast<const f32x4 *>(ap + m * 32 * kLd + 8 * ga);
-#pragma unroll
-  for (int j = 0; j < NR; ++j) f.b[j] = bp[j][(size_t)gb * 64];
-}
-
 // A wave's weight stream over one layer operand through a buffer descriptor
 // (wave-uniform base and size): each load is one buffer_load_dwordx4 with the
 // lane's column-tile offset in a VGPR fixed for the layer and the 1 KiB block
@@ -203,7 +179,13 @@ __device__ __forceinline__ T wload(const WStream<NR> &w, int j, int blk) {
   return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.vo[j], blk * 1024, 0));
 }
 
-template <int MR, int NR>
+// TR: weights as the A operand and activations as B, so the accumulator holds
+// C^T -- a lane owns one point (column lane & 31) and 16 of its outputs
+// (rows (q & 3) + 8 (q >> 2) + 4 (lane >> 5)), four runs of four consecutive
+// features: the epilogue writes them with ds_write_b128 (layer_store).  The A
+// and B fragment layouts of 32x32 MFMAs are the same, so only the operand
+// order changes.
+template <int MR, int NR, bool TR>
 __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[MR][NR]) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -211,7 +193,8 @@ __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[M
     for (int j = 0; j < NR; ++j) {
 #pragma unroll
       for (int m = 0; m < MR; ++m)
-        acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[m][s], f.b[j][s], acc[m][j], 0, 0, 0);
+        acc[m][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(f.b[j][s], f.a[m][s], acc[m][j], 0, 0, 0)
+                       : __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[m][s], f.b[j][s], acc[m][j], 0, 0, 0);
     }
   }
 }
@@ -228,29 +211,46 @@ __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[M
 #define IKHIP_ANN_RING 4
 #endif
 constexpr int kRing = IKHIP_ANN_RING;
-#ifndef IKHIP_ANN_BUF
-#define IKHIP_ANN_BUF 1
-#endif
 
+// The accumulators of a transposed (TR) layer start at the bias of their
+// features, times `scale` (the fp16x3 weight pre-scale, undone with the
+// products); Keras adds it after the dot product (ann.py:46-56), a change of
+// summation order within the fp32 tolerance.
 template <int MR, int NR>
+__device__ __forceinline__ void acc_init_bias(f32x16 (&acc)[MR][NR], const float *bias, int nt0,
+                                              int nt_stride, int lane, float scale = 1.0f) {
+  const int h = lane >> 5;
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const float *b = bias + (nt0 + nt_stride * j) * 32 + 4 * h;
+    f32x16 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const f32x4 q = *reinterpret_cast<const f32x4 *>(b + 8 * i) * scale;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) v[4 * i + t] = q[t];
+    }
+#pragma unroll
+    for (int m = 0; m < MR; ++m) acc[m][j] = v;
+  }
+}
+
+template <int MR, int NR, bool TR>
 __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restrict__ wp, int G,
                                            int wbytes, int g0, int g1, int nt0, int nt_stride,
-                                           int lane, f32x16 (&acc)[MR][NR]) {
+                                           int lane, const float *bias, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 4 * h;
+  if (TR) {
+    acc_init_bias(acc, bias, nt0, nt_stride, lane);
+  } else {
 #pragma unroll
-  for (int j = 0; j < NR; ++j)
+    for (int j = 0; j < NR; ++j)
 #pragma unroll
-    for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
+      for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
+  }
   if (g1 <= g0) return;
   Frag<MR, NR> f[kRing];
-#if IKHIP_ANN_BUF
-  // The weight stream through a buffer descriptor over the layer (wave-uniform
-  // base and size): each load is one buffer_load_dwordx4 with the lane's tile
-  // offset in a VGPR fixed for the layer, the group in an SGPR and the ring
-  // slot in the immediate offset -- no per-load 64-bit address arithmetic.
-  // Groups past the layer's end read zeros (range check); groups past a
-  // tile's K range read the next tile's data, which is never multiplied.
   const WStream<NR> ws = make_wstream<NR>(wp, wbytes, nt0, nt_stride, G, lane);
   auto load_b = [&](Frag<MR, NR> &fr, int gbase, int u) {
 #pragma unroll
@@ -278,44 +278,25 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
       load_a(f[(u + kRing - 1) % kRing], a0, u);
       load_b(f[(u + kRing - 1) % kRing], g + kRing - 1, u);
       __builtin_amdgcn_sched_barrier(0);
-      mma_group(f[u], acc);
+      mma_group<MR, NR, TR>(f[u], acc);
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-#else
-  (void)wbytes;
-  const int last = g1 - 1;
-  const f32x4 *bp[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) bp[j] = wp + (size_t)(nt0 + nt_stride * j) * G * 64 + lane;
-#pragma unroll
-  for (int u = 0; u < kRing - 1; ++u) load_group(f[u], ap, bp, min(g0 + u, last));
-  int g = g0;
-  for (; g + kRing <= g1; g += kRing) {
-#pragma unroll
-    for (int u = 0; u < kRing; ++u) {
-      load_group(f[(u + kRing - 1) % kRing], ap, bp, min(g + u + kRing - 1, last));
-      __builtin_amdgcn_sched_barrier(0);
-      mma_group(f[u], acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#endif
 #pragma unroll
   for (int u = 0; u < kRing - 1; ++u)
-    if (g + u < g1) mma_group(f[u], acc);
+    if (g + u < g1) mma_group<MR, NR, TR>(f[u], acc);
 }
 
-// C/D map of the 32x32 MFMA: column lane & 31, row (q & 3) + 8 (q >> 2) + 4 (lane >> 5).
-// bv[j]: the bias of the lane's column in tile j, loaded before the GEMM (a
-// load issued here, after the barrier, would put a memory round trip on every
-// layer's critical path).  The activation runs on 8 elements at a time, phase
-// by phase, so the dependent exp / rcp chains of different elements overlap
-// (one element pair at a time, each step waiting on the last, cost ~100 cycles
-// per pair).
+// Epilogue of a full-width fp32 layer (C layout: column lane & 31, rows
+// (q & 3) + 8 (q >> 2) + 4 (lane >> 5)).  bv[j]: the bias of the lane's column
+// in tile j, loaded before the GEMM (a load issued here, after the barrier,
+// would put a memory round trip on every layer's critical path).  The
+// transposed form below (bias in the accumulators, b128 stores) measured
+// 0.6 k cycles per layer slower here: its 5.9 k-cycle epilogue saves 0.7 k,
+// its GEMM loses 1.3 k (bias loads ahead of the first MFMA).
 template <int MR, int NR, int ACT>
-__device__ __forceinline__ void layer_store(float *H, const float (&bv)[NR], int wave, int lane,
-                                            f32x16 (&acc)[MR][NR], unsigned long long *st) {
+__device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], int wave, int lane,
+                                              f32x16 (&acc)[MR][NR], unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
   stamp(st);
   __syncthreads();  // every wave has finished reading the layer input
@@ -339,6 +320,38 @@ __device__ __forceinline__ void layer_store(float *H, const float (&bv)[NR], int
           H[(row + 1) * kLd + col] = t[k].y;
         }
       }
+  }
+}
+
+// Epilogue of a full-width split-mode layer on the transposed tile (mma_group TR): the
+// lane's point is row m * 32 + (lane & 31) of H, its 16 features four runs of
+// four at columns 32 nt + 8 i + 4 (lane >> 5), each one ds_write_b128; the bias
+// is already in the accumulators.  The activation runs on 8 elements at a
+// time, phase by phase, so the dependent exp / rcp chains of different
+// elements overlap (one element pair at a time, each step waiting on the last,
+// cost ~100 cycles per pair).  bf16x6 / fp16x3: 2-3 % faster than the C layout.
+template <int MR, int NR, int ACT>
+__device__ __forceinline__ void layer_store(float *H, int wave, int lane, f32x16 (&acc)[MR][NR],
+                                            unsigned long long *st) {
+  const int r = lane & 31, h = lane >> 5;
+  stamp(st);
+  __syncthreads();  // every wave has finished reading the layer input
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const int col0 = (wave + kWaves * j) * 32 + 4 * h;
+#pragma unroll
+    for (int m = 0; m < MR; ++m) {
+      float *row = H + (m * 32 + r) * kLd + col0;
+#pragma unroll
+      for (int q0 = 0; q0 < 16; q0 += 8) {
+        f32x2 t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = f32x2{acc[m][j][q0 + 2 * k], acc[m][j][q0 + 2 * k + 1]};
+        act_apply2x4<ACT>(t);
+        *reinterpret_cast<f32x4 *>(row + 2 * q0) = f32x4{t[0].x, t[0].y, t[1].x, t[1].y};
+        *reinterpret_cast<f32x4 *>(row + 2 * q0 + 8) = f32x4{t[2].x, t[2].y, t[3].x, t[3].y};
+      }
+    }
   }
 }
 
@@ -432,12 +445,12 @@ __device__ __forceinline__ void step_x(Split3 (&sa)[MR], const WStep<NR> &w, WSt
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       f32x16 c = acc[m][j];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].lo, w.p[j][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].mid, w.p[j][1], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].hi, w.p[j][2], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].mid, w.p[j][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].hi, w.p[j][1], c, 0, 0, 0);
-      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sa[m].hi, w.p[j][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][0], sa[m].lo, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][1], sa[m].mid, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][2], sa[m].hi, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][0], sa[m].mid, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][1], sa[m].hi, c, 0, 0, 0);
+      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][0], sa[m].hi, c, 0, 0, 0);
     }
   // issue order: the loads, a few MFMAs to cover the LDS latency, then the
   // split VALU two instructions per MFMA gap
@@ -460,13 +473,10 @@ __device__ __forceinline__ void step_x(Split3 (&sa)[MR], const WStep<NR> &w, WSt
 template <int MR, int NR>
 __device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__restrict__ wx,
                                              int G16, int xbytes, int wave, int lane,
-                                             f32x16 (&acc)[MR][NR]) {
+                                             const float *bias, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 8 * h;
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
+  acc_init_bias(acc, bias, wave, kWaves, lane);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 3, lane);
   WStep<NR> w0, w1, w2;
   load_w(w0, ws, 0);
@@ -556,9 +566,9 @@ __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WS
 #pragma unroll
     for (int j = 0; j < NR; ++j) {
       f32x16 c = acc[m][j];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[m].lo, w.p[j][0], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[m].hi, w.p[j][1], c, 0, 0, 0);
-      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(sa[m].hi, w.p[j][0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][0], sa[m].lo, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][1], sa[m].hi, c, 0, 0, 0);
+      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][0], sa[m].hi, c, 0, 0, 0);
     }
   constexpr int kMfma = 3 * MR * NR, kLead = (kMfma >= 12) ? 6 : kMfma / 2;
   __builtin_amdgcn_sched_group_barrier(0x020, 2 * NR, 0);  // VMEM reads
@@ -578,13 +588,10 @@ __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WS
 template <int MR, int NR>
 __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__restrict__ wx,
                                              int G16, int xbytes, float xinv, int wave, int lane,
-                                             f32x16 (&acc)[MR][NR]) {
+                                             const float *bias, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 8 * h;
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
+  acc_init_bias(acc, bias, wave, kWaves, lane, 1.0f / xinv);  // exact: xinv is 2^-k
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 2, lane);
   WStepH<NR> w0, w1, w2;
   load_wh(w0, ws, 0);
@@ -621,23 +628,31 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
                                           const void *wx = nullptr, int G16 = 0,
                                           float xinv = 1.0f) {
   f32x16 acc[MR][NR];
+  const int NT = wbytes / (G * 1024);  // column tiles of the layer
+  if (X != 0 && wx) {
+    if (X == 1)
+      layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024, wave,
+                           lane, bias, acc);
+    else
+      layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024, xinv,
+                           wave, lane, bias, acc);
+    switch (act) {
+      case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, wave, lane, acc, st); break;
+      case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, wave, lane, acc, st); break;
+      case IK_ACT_SIGMOID: layer_store<MR, NR, IK_ACT_SIGMOID>(H, wave, lane, acc, st); break;
+      default: layer_store<MR, NR, IK_ACT_LINEAR>(H, wave, lane, acc, st); break;
+    }
+    return;
+  }
   float bv[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + kWaves * j) * 32 + (lane & 31)];
-  const int NT = wbytes / (G * 1024);  // column tiles of the layer
-  if (X == 1 && wx)
-    layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024, wave,
-                         lane, acc);
-  else if (X == 2 && wx)
-    layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024, xinv,
-                         wave, lane, acc);
-  else
-    layer_gemm<MR, NR>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, acc);
+  layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, nullptr, acc);
   switch (act) {
-    case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, bv, wave, lane, acc, st); break;
-    case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, bv, wave, lane, acc, st); break;
-    case IK_ACT_SIGMOID: layer_store<MR, NR, IK_ACT_SIGMOID>(H, bv, wave, lane, acc, st); break;
-    default: layer_store<MR, NR, IK_ACT_LINEAR>(H, bv, wave, lane, acc, st); break;
+    case IK_ACT_TANH: layer_store_c<MR, NR, IK_ACT_TANH>(H, bv, wave, lane, acc, st); break;
+    case IK_ACT_RELU: layer_store_c<MR, NR, IK_ACT_RELU>(H, bv, wave, lane, acc, st); break;
+    case IK_ACT_SIGMOID: layer_store_c<MR, NR, IK_ACT_SIGMOID>(H, bv, wave, lane, acc, st); break;
+    default: layer_store_c<MR, NR, IK_ACT_LINEAR>(H, bv, wave, lane, acc, st); break;
   }
 }
 
@@ -662,7 +677,7 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
   constexpr int BM = 32 * MR;
   f32x16 acc[MR][1];
   const int g0 = (G * wave) / kWaves, g1 = (G * (wave + 1)) / kWaves;
-  layer_gemm<MR, 1>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, acc);
+  layer_gemm<MR, 1, false>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, nullptr, acc);
   stamp(st);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
