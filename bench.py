@@ -55,6 +55,8 @@ def parse():
                     help="ANN hidden-GEMM arithmetic of the headline line (ikhip.h "
                          "ik_ann_set_mode); the other mode is reported under 'secondary'")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01", "pmc"),
+                    help="committed PMC diagnosis summaries (pipe occupancy in the roofline)")
     ap.add_argument("--gather", type=int, default=0,
                     help="N>1: include the RCCL all_gather of every rank's angle rows in the "
                          "timed step (delivers the whole batch to every rank)")
@@ -127,6 +129,24 @@ def load_traffic(path, kernel):
         return None
 
 
+def load_pipe(path, kernel):
+    """Pipe occupancy of `kernel` from the committed PMC diagnosis pass
+    (tools/pmc_diag.sh -> tools/pmc_summary.py): MFMA busy, VALU active and
+    fp64-pipe busy as fractions of the kernel's SIMD cycles; None if absent."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for k, v in d.items():
+        if k.split("<")[0] == kernel:
+            return {"mfma_busy": v.get("MfmaUtil_pct", 0.0) / 100,
+                    "valu_active": v.get("ValuActive_pct", 0.0) / 100,
+                    "fp64_pipe_busy": v.get("Fp64PipeBusy_pct", 0.0) / 100,
+                    "source": os.path.relpath(path, ROOT)}
+    return None
+
+
 def make_gather(dang, args, world):
     """The optional delivery step: all_gather of the per-rank angle rows over
     RCCL (inversekinematicsann_amd.dist.gather_rows), on the solve's stream."""
@@ -185,6 +205,9 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
                        "points_per_launch": n}
     if mode == "fp32":
+        res["roofline"]["pipes"] = load_pipe(os.path.join(args.pmc_dir, "ann_diag_summary.json"),
+                                             "ann_fused_kernel")
+    if mode == "fp32":
         res["dtype"] = "fp32"
         res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
                            f"{_pts(n)} random_dist points per GPU")
@@ -231,7 +254,12 @@ def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
                        "frac": achieved / FP64_VALU_PEAK if achieved else None,
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
-                       "iterations_per_launch": int(st.sum_iters)}
+                       "iterations_per_launch": int(st.sum_iters),
+                       # the flop count prices a correctly rounded sqrt / division as
+                       # one flop; the pipes say how busy the SIMDs actually are
+                       "pipes": load_pipe(os.path.join(args.pmc_dir,
+                                                       "fabrik_diag_summary.json"),
+                                          "fabrik_iter_kernel")}
     res["dtype"] = "f64"
     res["workload"] = (f"FABRIK ikine (seed FK + loop + angles), tol {tol:g} / "
                        f"{max_iter} iterations, float64, {_pts(n)} random_dist points per GPU")

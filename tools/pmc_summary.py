@@ -26,8 +26,17 @@ def main(dirs):
     out = {}
     for k, cs in tot.items():
         avg = {c: v / max(1, len(disp[k][c])) for c, v in cs.items()}
-        if "GRBM_GUI_ACTIVE" in avg and "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
-            avg["MfmaUtil_pct"] = 100 * avg["SQ_VALU_MFMA_BUSY_CYCLES"] / (avg["GRBM_GUI_ACTIVE"] * 1024)
+        # GRBM_GUI_ACTIVE is summed over the 8 XCDs: /8 is the kernel's cycles;
+        # the SQ counters are summed over the 1024 SIMDs (MI355X_MICROARCH.md)
+        simd_cycles = avg.get("GRBM_GUI_ACTIVE", 0.0) / 8 * 1024
+        if simd_cycles and "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+            avg["MfmaUtil_pct"] = 100 * avg["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+        if simd_cycles and "SQ_ACTIVE_INST_VALU" in avg:  # quad-cycles
+            avg["ValuActive_pct"] = 100 * 4 * avg["SQ_ACTIVE_INST_VALU"] / simd_cycles
+        f64 = [avg.get(f"SQ_INSTS_VALU_{o}_F64") for o in ("ADD", "MUL", "FMA")]
+        if simd_cycles and all(v is not None for v in f64):
+            # a wave64 fp64 add / mul / fma occupies the SIMD's fp64 pipe 4 cycles
+            avg["Fp64PipeBusy_pct"] = 100 * 4 * sum(f64) / simd_cycles
         if "TCC_HIT_sum" in avg and "TCC_MISS_sum" in avg:
             avg["L2_hit_pct"] = 100 * avg["TCC_HIT_sum"] / max(1, avg["TCC_HIT_sum"] + avg["TCC_MISS_sum"])
         out[k] = avg
