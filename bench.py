@@ -318,6 +318,20 @@ def end_to_end(solve_host, dpts, args, world):
             "unit": "IK solutions/s", "path": "host pointers (ik_*_solve without IK_F_DEVICE)"}
 
 
+def _host_cpu():
+    """The GPU host's CPU (record the model and os.cpu_count())."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "os_cpu_count": os.cpu_count()}
+
+
 def cpu_baseline(method, args, sample_pts=None, gpu_out=None):
     """The oracle timed on this host (rank 0, N=1) over a bounded sample, which
     is the first points of the GPU batch: the oracle's results on it are also
@@ -348,6 +362,7 @@ def cpu_baseline(method, args, sample_pts=None, gpu_out=None):
                 break
         el = time.perf_counter() - t0
         res = {"value": done / el, "unit": "IK solutions/s", "cores": threads, "kind": "port",
+               "host_cpu": _host_cpu(),
                "sample": f"{done} points (the GPU batch's first {chunk}, repeated) in "
                          f"{chunk}-point batches, numpy fp32 MLP (oracle.ann_forward) on "
                          f"{threads} BLAS threads, {el:.1f} s"}
@@ -368,6 +383,7 @@ def cpu_baseline(method, args, sample_pts=None, gpu_out=None):
             break
     el = time.perf_counter() - t0
     res = {"value": done / el, "unit": "IK solutions/s", "cores": 1, "kind": "port",
+           "host_cpu": _host_cpu(),
            "sample": f"{done} points (the GPU batch's first {chunk}, repeated), C oracle "
                      f"(oracle/ik_oracle.c, scalar, 1 thread), tol {args.tol:g}/{args.max_iter}, "
                      f"{el:.1f} s"}

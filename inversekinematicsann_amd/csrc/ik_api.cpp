@@ -194,11 +194,11 @@ int ik_ctx_create(int device, ik_ctx **out) {
   if (e == hipSuccess) e = hipMalloc(&c->fab_ord, sizeof(FabOrderDev));
   if (e == hipSuccess) e = hipMemset(c->fab_ord, 0, sizeof(FabOrderDev));
   if (e == hipSuccess) e = hipMalloc(&c->rconst, sizeof(RobotConstDev));
+  c->stream = c->own_stream;
   if (e != hipSuccess) {
-    delete c;
+    (void)ik_ctx_destroy(c);  // frees whatever was allocated
     return fail(IK_E_HIP, std::string("ik_ctx_create: ") + hipGetErrorString(e));
   }
-  c->stream = c->own_stream;
   std::memcpy(c->robot.dh, kDefaultDh, sizeof(kDefaultDh));
   std::memcpy(c->robot.links, kDefaultLinks, sizeof(kDefaultLinks));
   std::memcpy(c->robot.lim, kDefaultLimits, sizeof(kDefaultLimits));
