@@ -238,7 +238,8 @@ __device__ __forceinline__ void acc_init_bias(f32x16 (&acc)[MR][NR], const float
 template <int MR, int NR, bool TR>
 __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restrict__ wp, int G,
                                            int wbytes, int g0, int g1, int nt0, int nt_stride,
-                                           int lane, const float *bias, f32x16 (&acc)[MR][NR]) {
+                                           int lane, const float *bias, f32x16 (&acc)[MR][NR],
+                                           unsigned long long *st_first = nullptr) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 4 * h;
   if (TR) {
@@ -280,6 +281,7 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
       __builtin_amdgcn_sched_barrier(0);
       mma_group<MR, NR, TR>(f[u], acc);
       __builtin_amdgcn_sched_barrier(0);
+      if (u == 0 && g == g0) stamp(st_first);  // diagnostic: first K group done
     }
   }
 #pragma unroll
@@ -625,6 +627,7 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
 template <int MR, int NR, int X = 0>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
+                                          unsigned long long *st_first,
                                           const void *wx = nullptr, int G16 = 0,
                                           float xinv = 1.0f) {
   f32x16 acc[MR][NR];
@@ -647,7 +650,7 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   float bv[NR];
 #pragma unroll
   for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + kWaves * j) * 32 + (lane & 31)];
-  layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, nullptr, acc);
+  layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, nullptr, acc, st_first);
   switch (act) {
     case IK_ACT_TANH: layer_store_c<MR, NR, IK_ACT_TANH>(H, bv, wave, lane, acc, st); break;
     case IK_ACT_RELU: layer_store_c<MR, NR, IK_ACT_RELU>(H, bv, wave, lane, acc, st); break;
@@ -776,6 +779,7 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
       const float *bias = a.m.bias[l];
       const int act = a.m.act[l];
       unsigned long long *sl = (stp && l < 14) ? stp + 2 + 2 * l : nullptr;
+      unsigned long long *sf = (stp && l == 5) ? stp + 30 : nullptr;  // layer 5's first group
       const void *wx = X ? a.m.wx[l] : nullptr;
       if (NT == 1) {
         run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid, sl);
@@ -784,19 +788,19 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
         const int G16 = (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
-          case 3: run_layer<MR, 3, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
-          case 2: run_layer<MR, 2, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
-          case 1: run_layer<MR, 1, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, wx, G16, xinv); break;
+          case 4: run_layer<MR, 4, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
+          case 3: run_layer<MR, 3, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
+          case 2: run_layer<MR, 2, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
+          case 1: run_layer<MR, 1, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
           default: __syncthreads(); break;
         }
       } else {
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
-          case 3: run_layer<MR, 3>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
-          case 2: run_layer<MR, 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
-          case 1: run_layer<MR, 1>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl); break;
+          case 4: run_layer<MR, 4>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 3: run_layer<MR, 3>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 2: run_layer<MR, 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 1: run_layer<MR, 1>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
           default: __syncthreads(); break;  // idle wave still joins the barrier
         }
       }

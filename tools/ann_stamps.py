@@ -41,5 +41,7 @@ for t in range(1, 4):
     row["gemm_per_layer_per_wave"] = gemm
     row["post_gemm_per_layer_per_wave"] = epi
     row["output"] = int(np.median(w[:, 31] - w[:, 3 + 2 * (L - 1)]))
+    if L > 5:  # slot 30: layer 5's first K group done (from layer 4 done)
+        row["layer5_first_group"] = [int(x) for x in w[:, 30] - w[:, 3 + 2 * 4]]
     res["per_tile"].append(row)
 print(json.dumps(res))
