@@ -1,0 +1,101 @@
+"""C-ABI argument checking on a live context (include/ikhip.h): every entry
+point refuses bad arguments with IK_E_BADARG / IK_E_NOMODEL and a message in
+ik_last_error(), leaves the context usable, and never launches a kernel on a
+rejected call.  The Python wrappers surface these as NativeError."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from inversekinematicsann_amd import _native
+    c = _native.Context(0)
+    yield c
+    c.close()
+
+
+def _rc_msg(ctx, rc):
+    return rc, ctx.lib.ik_last_error().decode()
+
+
+def test_bad_arguments_are_refused(ctx):
+    from inversekinematicsann_amd import _native as N
+    L, h = ctx.lib, ctx.handle
+    st = N.IkStats()
+    pts = np.zeros((4, 3))
+    ang = np.zeros((4, 4))
+    # negative sizes / null pointers
+    rc, msg = _rc_msg(ctx, L.ik_fabrik_solve(h, pts.ctypes.data, -1, 1e-3, 100, ang.ctypes.data,
+                                             None, None, 0, ctypes.byref(st)))
+    assert rc == N.IK_E_BADARG and "ik_fabrik_solve" in msg
+    rc, msg = _rc_msg(ctx, L.ik_fabrik_solve(h, None, 4, 1e-3, 100, ang.ctypes.data, None, None,
+                                             0, ctypes.byref(st)))
+    assert rc == N.IK_E_BADARG
+    rc, msg = _rc_msg(ctx, L.ik_fk(h, ang.ctypes.data, 4, None, None, 0, ctypes.byref(st)))
+    assert rc == N.IK_E_BADARG and "ik_fk" in msg
+    rc, msg = _rc_msg(ctx, L.ik_check_limits(h, None, 3, 0, ctypes.byref(st)))
+    assert rc == N.IK_E_BADARG
+    # async without device pointers
+    rc, msg = _rc_msg(ctx, L.ik_fabrik_solve(h, pts.ctypes.data, 4, 1e-3, 100, ang.ctypes.data,
+                                             None, None, N.IK_F_ASYNC, ctypes.byref(st)))
+    assert rc == N.IK_E_BADARG and "IK_F_ASYNC" in msg
+    # generic chains: 2..8 joints only
+    with pytest.raises(N.NativeError) as ei:
+        ctx.fabrik_calc(np.ones(9), np.zeros((9, 3)), np.zeros((2, 3)))
+    assert ei.value.code == N.IK_E_BADARG
+    # unknown ANN mode
+    rc, msg = _rc_msg(ctx, L.ik_ann_set_mode(h, 7))
+    assert rc == N.IK_E_BADARG and "mode" in msg
+    # the context still works
+    p = np.array([[1.0, 2.1, 3.0]])
+    a, it, _, s = ctx.fabrik_solve(p)
+    ra, rit, _, _ = O.fabrik_ikine(p)
+    assert np.array_equal(it, rit) and np.abs(a - ra).max() <= 1e-9
+
+
+def test_ann_without_model_and_bad_models():
+    from inversekinematicsann_amd import _native as N
+    from inversekinematicsann_amd.kinematics.ann import REFERENCE_X_SCALER as XS, \
+        REFERENCE_Y_SCALER as YS
+    c = N.Context(0)
+    try:
+        with pytest.raises(N.NativeError) as ei:
+            c.ann_solve(np.zeros((3, 3)))
+        assert ei.value.code == N.IK_E_NOMODEL
+        rng = np.random.default_rng(0)
+
+        def dense(i, o):
+            return rng.standard_normal((i, o)).astype(np.float32), np.zeros(o, np.float32)
+
+        # too wide (the LDS tile holds 512 features), wrong input / output widths
+        for dims in ((3, 600, 4), (4, 16, 4), (3, 16, 5)):
+            ws, bs = zip(*[dense(dims[k], dims[k + 1]) for k in range(len(dims) - 1)])
+            with pytest.raises(N.NativeError) as ei:
+                c.ann_load(list(ws), list(bs), ["tanh"] * (len(dims) - 2) + ["linear"], XS.mean,
+                           XS.scale, YS.mean, YS.scale)
+            assert ei.value.code == N.IK_E_BADARG
+        # after the refusals a valid model loads and solves
+        ws, bs = zip(*[dense(3, 32), dense(32, 4)])
+        c.ann_load(list(ws), list(bs), ["tanh", "linear"], XS.mean, XS.scale, YS.mean, YS.scale)
+        pts = np.array([[1.0, 0.5, 2.0], [0.3, -0.2, 1.0]])
+        ang, _, _ = c.ann_solve(pts)
+        ref = O.ann_forward(pts, list(ws), list(bs), ["tanh", "linear"], XS.mean, XS.scale,
+                            YS.mean, YS.scale)
+        assert np.abs(ang.astype(np.float64) - ref).max() <= 1e-5
+    finally:
+        c.close()
+
+
+def test_bad_device_index():
+    from inversekinematicsann_amd import _native as N
+    L = N.load_library()
+    h = ctypes.c_void_p()
+    rc = L.ik_ctx_create(4096, ctypes.byref(h))
+    assert rc == N.IK_E_BADARG and not h.value
+    assert b"out of range" in L.ik_last_error()
