@@ -700,10 +700,13 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     kt_end(stream);
   }
   // persistent grid: blocks_per_cu 256-thread blocks per CU (= waves per SIMD)
-  // measured on MI355X at 1M points (tools/sweep_fabrik.py): 2 blocks/CU with
-  // 64-point grabs beats 4 and 8 (more lanes = fewer points per lane = a
-  // longer divergent tail) by 10-30 %.
-  static const int bpc = env_int("IKHIP_FABRIK_BPC", 2);
+  // measured on MI355X (tools/sweep_fabrik.py): at 1M points 2 blocks/CU with
+  // 64-point grabs beats 4 and 8 by 10-30 % (more lanes = fewer points per lane
+  // = a longer divergent tail); 2 and 3 are within noise at 1-1.25M points, and
+  // from 4M points on 3 wins by ~5 % at every tolerance (the tail matters less
+  // than the latency a third wave per SIMD hides).
+  static const int bpc_env = env_int("IKHIP_FABRIK_BPC", 0);
+  const int bpc = bpc_env > 0 ? bpc_env : (n >= 2000000 ? 3 : 2);
   static const int chunk = env_int("IKHIP_FABRIK_CHUNK", 64);
   a.chunk = chunk > 0 ? chunk : 64;
   unsigned pgrid = (unsigned)num_cus() * (unsigned)(bpc > 0 ? bpc : 8);

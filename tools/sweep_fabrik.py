@@ -45,6 +45,9 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "grid":  # persistent-grid size, ordered pipeline
         for bpc in ("2", "3", "4"):
             cases.append({"IKHIP_FABRIK_BPC": bpc})
+    if len(sys.argv) > 1 and sys.argv[1] == "bpc":  # grid size across tolerances / sizes
+        for bpc in ("2", "3", "4"):
+            cases.append({"IKHIP_FABRIK_BPC": bpc})
     if len(sys.argv) > 1 and sys.argv[1] == "core":  # sqrt/div core sequences on/off x grid
         for core in ("0", "1"):
             for bpc in ("2", "3", "4"):
@@ -57,7 +60,9 @@ if __name__ == "__main__":
                 cases.append({"IKHIP_FABRIK_VARIANT": var, "IKHIP_FABRIK_BPC": bpc,
                               "IKHIP_FABRIK_CHUNK": chunk})
     n_pts = int(os.environ.get("SWEEP_N", "1000000"))
-    for n, tol, mi in ((n_pts, 1e-3, 100), (n_pts, 1e-5, 200)):
+    tols = [(float(t.split("/")[0]), int(t.split("/")[1]))
+            for t in os.environ.get("SWEEP_TOLS", "1e-3/100,1e-5/200").split(",")]
+    for n, tol, mi in [(n_pts, t, m) for t, m in tols]:
         for c in cases:
             r = run(c, n, tol, mi)
             tot = sum(v for v in r.values() if isinstance(v, float))
