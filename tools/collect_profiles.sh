@@ -8,14 +8,17 @@ OUT=gpurun_out
 DST=profiles/$R
 mkdir -p $DST/pmc
 for m in ann fabrik ann_bf16x6 ann_fp16x3; do
-  cp $OUT/prof_stats_$m/*/*_kernel_stats.csv $DST/${m}_kernel_stats.csv
+  # gpurun_out/ accumulates the runs of earlier calls: take the newest
+  cp "$(ls -t $OUT/prof_stats_$m/*/*_kernel_stats.csv | head -1)" $DST/${m}_kernel_stats.csv
   for c in fetch write; do
     python - "$OUT/prof_${c}_$m" "$DST/pmc/${m}_${c}_summary.csv" <<'PY'
 import csv, glob, os, sys
 from collections import defaultdict
 src, dst = sys.argv[1], sys.argv[2]
 tot, disp = defaultdict(float), defaultdict(set)
-for f in glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True):
+files = sorted(glob.glob(os.path.join(src, "**", "*counter_collection.csv"), recursive=True),
+               key=os.path.getmtime)
+for f in files[-1:]:  # the newest run only
     for row in csv.DictReader(open(f)):
         key = (row["Kernel_Name"][:80], row["Counter_Name"])
         tot[key] += float(row["Counter_Value"])
