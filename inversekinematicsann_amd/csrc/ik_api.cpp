@@ -81,7 +81,7 @@ struct ik_ctx {
   float ann_hinv[kAnnMaxLayers] = {};      // fp16x3: 2^-(weight pre-scale exponent)
   int ann_mode = IK_ANN_FP32;
   int fabrik_variant = 1;
-  int fabrik_core = 1;  // IKHIP_FABRIK_CORE: sqrt_core / div_core iteration (ik_common.h)
+  int fabrik_core = 2;  // IKHIP_FABRIK_CORE: 2 core + reuse, 1 sqrt_core / div_core, 0 general
   KTimer kt;
   unsigned long long *dbg = nullptr;  // diagnostic stamp buffer (ik_ctx_set_debug)
   FabOrderDev *fab_ord = nullptr;     // FABRIK work-order cost table (learned per robot)
@@ -424,7 +424,7 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
   launch_reset_stats(c->d_stats, c->stream);
   launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj,
                       !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
-                      c->fabrik_variant, c->fabrik_core != 0, c->fab_ord, c->rconst,
+                      c->fabrik_variant, c->fabrik_core, c->fab_ord, c->rconst,
                       c->dbg);
   IK_HIP(hipGetLastError());
   if (!dev && n > 0) {

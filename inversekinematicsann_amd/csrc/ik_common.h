@@ -397,7 +397,7 @@ size_t fabrik_scratch_bytes(int64_t n);
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t st,
-                         int variant, bool core, FabOrderDev *ord, const RobotConstDev *rc,
+                         int variant, int core, FabOrderDev *ord, const RobotConstDev *rc,
                          unsigned long long *dbg);
 constexpr size_t kFabrikDebugWords = 64 + 4 * 4000;  // diagnostic build counters
 // Per-robot seed constants (RobotConstDev) into device memory, on stream st.

@@ -55,6 +55,55 @@ __device__ __forceinline__ void fabrik_step4_core(const d3 start, d3 &c1, d3 &c2
   ge2 = dist3_sq(c3, g);
 }
 
+// fabrik_step4_core with the two distances the reference computes twice taken once
+// (links L0 == L1 and L2 == L3, bitwise; the host checks):
+//  * b0 = pb(b1, start, L0) and c1 = pb(start, b1, L1) share |b1 - start| (the
+//    radicand squares start - b1 = -(b1 - start) exactly) and, with L0 == L1, the
+//    quotient, so c1 = start + q*(b1 - start) = start - q*(start - b1);
+//  * this iteration's c3 = pb(c2, g, L3) and the next one's b2 = pb(g, c2, L2) share
+//    |c2 - g| and, with L2 == L3, the quotient: the lane carries (cq, cd = g - c2)
+//    into the next iteration, whose b2 = g + cq*(c2 - g) = g - cq*cd.
+// Every value is the one the reference computes (IEEE: a + (-b) == a - b and
+// q*(-d) == -(q*d)), so the bits do not change; two of the six square roots and
+// divisions per iteration go.  cdom is the carried radicand's domain value: it joins
+// dom so that the wave-uniform fallback still sees it.
+__device__ __forceinline__ void fabrik_step4_reuse(const d3 start, d3 &c1, d3 &c2, d3 &c3,
+                                                   const d3 g, const double *L, double &se2,
+                                                   double &ge2, double &cq, d3 &cd,
+                                                   uint32_t &cdom, uint32_t &dom) {
+  dom = cdom;
+  const d3 b2 = {g.x - cq * cd.x, g.y - cq * cd.y, g.z - cq * cd.z};
+  const d3 b1 = point_between_core(b2, c1, L[1], dom);
+  const double dx = start.x - b1.x, dy = start.y - b1.y, dz = start.z - b1.z;
+  const double x = sq(dx) + sq(dy) + sq(dz);
+  dom = max(dom, sqrt_core_dom(x));
+  const double q = div_core(L[0], sqrt_core(x));
+  const d3 b0 = {b1.x + (q * dx), b1.y + (q * dy), b1.z + (q * dz)};
+  se2 = dist3_sq(b0, start);
+  c1 = {start.x - (q * dx), start.y - (q * dy), start.z - (q * dz)};
+  c2 = point_between_core(c1, b2, L[2], dom);
+  const double ex = g.x - c2.x, ey = g.y - c2.y, ez = g.z - c2.z;
+  const double x3 = sq(ex) + sq(ey) + sq(ez);
+  cdom = sqrt_core_dom(x3);
+  dom = max(dom, cdom);
+  cq = div_core(L[3], sqrt_core(x3));
+  c3 = {c2.x + (cq * ex), c2.y + (cq * ey), c2.z + (cq * ez)};
+  cd = {ex, ey, ez};
+  ge2 = dist3_sq(c3, g);
+}
+
+// The carry of fabrik_step4_reuse for a chain whose c2 did not come from it (a
+// refilled lane's seed pose, or the general step of a fallback), through the
+// general sqrt / division: the same bits inside sqrt_core's domain, and outside it
+// cdom sends the next iteration to the fallback, which recomputes everything.
+__device__ __forceinline__ void reuse_carry(const d3 c2, const d3 g, double L3, double &cq,
+                                            d3 &cd, uint32_t &cdom) {
+  cd = {g.x - c2.x, g.y - c2.y, g.z - c2.z};
+  const double x = sq(cd.x) + sq(cd.y) + sq(cd.z);
+  cdom = sqrt_core_dom(x);
+  cq = L3 / sqrt(x);
+}
+
 // div_core's domain for the link lengths (the numerators): 2^-100 <= |L| <= 2^100.
 static bool links_core_ok(const double *L, int n) {
   for (int k = 0; k < n; ++k) {
@@ -410,7 +459,9 @@ __global__ __launch_bounds__(256) void fabrik_order_scatter_kernel(FabArgs a) {
 // ORD: the queue is a.perm (work order above): a refilled lane gathers its
 // point's seed pose and goal, and writes its results at its queue position,
 // which the angles kernel maps back to the point.
-template <int REFILL_MIN, bool ORD, bool CORE>
+// CORE: 0 general sqrt / division, 1 sqrt_core / div_core, 2 the same with the
+// repeated distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
+template <int REFILL_MIN, bool ORD, int CORE>
 __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -425,6 +476,9 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   d3 J0 = {0, 0, 0}, J1 = J0, J2 = J0, J3 = J0, g = J0;
   double se = 1.0, ge = 1.0;
   int step = 0, st = IK_OK;
+  double cq = 0.0;  // CORE == 2: the carried quotient, offset and domain value
+  d3 cd = J0;
+  uint32_t cdom = 0;
 
 #ifdef IKHIP_DIAG
   unsigned long long dg[kDiagCount] = {};
@@ -476,6 +530,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
           st = a.status[idx];
         }
         J0 = Jn[0]; J1 = Jn[1]; J2 = Jn[2]; J3 = Jn[3];
+        if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
         se = 1.0;
         ge = 1.0;
         step = 0;
@@ -496,7 +551,24 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
 #endif
     if (active) {
       if (st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step)) {
-        if constexpr (CORE) {
+        if constexpr (CORE == 2) {
+          uint32_t dom = 0, cdom_n = cdom;
+          d3 n1 = J1, n2 = J2, n3 = J3, cd_n = cd;
+          double se_n, ge_n, cq_n = cq;
+          fabrik_step4_reuse(J0, n1, n2, n3, g, L, se_n, ge_n, cq_n, cd_n, cdom_n, dom);
+          if (__all(dom < kCoreDom)) {
+            J1 = n1; J2 = n2; J3 = n3;
+            se = se_n;
+            ge = ge_n;
+            cq = cq_n;
+            cd = cd_n;
+            cdom = cdom_n;
+          } else {
+            IKHIP_DG(kDiagFallbacks, 1);
+            fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
+            reuse_carry(J2, g, L[3], cq, cd, cdom);
+          }
+        } else if constexpr (CORE == 1) {
           // wave-uniform fallback: when any lane's radicand leaves sqrt_core's
           // domain (coincident joints, non-finite input) the wave redoes the
           // iteration with the general sqrt / division (and their errors)
@@ -607,19 +679,22 @@ static int num_cus() {
 }
 
 template <int REFILL_MIN, bool ORD>
-static void launch_iter(bool core, unsigned grid, hipStream_t stream, const FabArgs &a) {
-  if (core)
-    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, true>), dim3(grid), dim3(256), 0,
+static void launch_iter(int core, unsigned grid, hipStream_t stream, const FabArgs &a) {
+  if (core == 2)
+    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, 2>), dim3(grid), dim3(256), 0,
+                       stream, a);
+  else if (core == 1)
+    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, 1>), dim3(grid), dim3(256), 0,
                        stream, a);
   else
-    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, false>), dim3(grid), dim3(256), 0,
+    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, 0>), dim3(grid), dim3(256), 0,
                        stream, a);
 }
 
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
-                         int variant, bool core_req, FabOrderDev *ord,
+                         int variant, int core_req, FabOrderDev *ord,
                          const RobotConstDev *rc, unsigned long long *dbg) {
   if (n <= 0) return;
   FabArgs a;
@@ -714,9 +789,13 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   if ((int64_t)pgrid * 4 > waves_needed)
     pgrid = (unsigned)((waves_needed + 3) / 4 > 0 ? (waves_needed + 3) / 4 : 1);
   // the iteration through sqrt_core / div_core (same bits, fewer instructions)
-  // unless the link lengths are outside div_core's domain; core_req = false
-  // (IKHIP_FABRIK_CORE=0 at context creation) forces the general sqrt / division.
-  const bool core = core_req && links_core_ok(a.r.links, 4);
+  // unless the link lengths are outside div_core's domain, and with the repeated
+  // distances taken once (core 2) when L0 == L1 and L2 == L3.  core_req (context's
+  // IKHIP_FABRIK_CORE) 0 forces the general sqrt / division, 1 the core sequences
+  // without the reuse.
+  const double *Lk = a.r.links;
+  int core = links_core_ok(Lk, 4) ? core_req : 0;
+  if (core == 2 && !(Lk[0] == Lk[1] && Lk[2] == Lk[3])) core = 1;
 #ifdef IKHIP_DIAG
   if (a.dbg) (void)hipMemsetAsync(a.dbg, 0, kFabrikDebugWords * 8, stream);
 #endif

@@ -326,7 +326,8 @@ def test_device_pointer_path(ctx1):
 
 
 def test_fabrik_core_sequences_bit_identical():
-    """The iteration kernel's sqrt_core / div_core path (ik_common.h) claims the
+    """The iteration kernel's sqrt_core / div_core path (ik_common.h), alone (1) and
+    with the repeated distances taken once (2, fabrik_step4_reuse), claims the
     same bits as the general sqrt / division wherever its domain check passes,
     and falls back per wave elsewhere: final joints and iteration counts of the
     two paths are compared bit for bit on reachable, unreachable (capped),
@@ -340,7 +341,7 @@ def test_fabrik_core_sequences_bit_identical():
     pts = np.concatenate([random_dist(200_000, seed=12), box, near,
                           [[0.0, 0.0, 2.0], [1e-300, 0.0, 2.0], [0.0, 0.0, 4.0]]])
     out = {}
-    for core in ("0", "1"):
+    for core in ("0", "1", "2"):
         os.environ["IKHIP_FABRIK_CORE"] = core
         c = _native.Context(0)
         os.environ.pop("IKHIP_FABRIK_CORE", None)
@@ -349,7 +350,8 @@ def test_fabrik_core_sequences_bit_identical():
                          for tol, mi in ((1e-3, 100), (1e-5, 200))]
         finally:
             c.close()
-    for (a0, i0, j0, s0), (a1, i1, j1, s1) in zip(out["0"], out["1"]):
+    pairs = list(zip(out["0"], out["1"])) + list(zip(out["0"], out["2"]))
+    for (a0, i0, j0, s0), (a1, i1, j1, s1) in pairs:
         assert np.array_equal(i0, i1)
         assert np.array_equal(j0.view(np.uint64), j1.view(np.uint64))
         assert np.array_equal(a0.view(np.uint64), a1.view(np.uint64))

@@ -48,10 +48,11 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "bpc":  # grid size across tolerances / sizes
         for bpc in ("2", "3", "4"):
             cases.append({"IKHIP_FABRIK_BPC": bpc})
-    if len(sys.argv) > 1 and sys.argv[1] == "core":  # sqrt/div core sequences on/off x grid
-        for core in ("0", "1"):
-            for bpc in ("2", "3", "4"):
-                cases.append({"IKHIP_FABRIK_CORE": core, "IKHIP_FABRIK_BPC": bpc})
+    if len(sys.argv) > 1 and sys.argv[1] == "core":  # iteration sequences x grid, twice
+        for _rep in range(2):
+            for core in os.environ.get("SWEEP_CORES", "1,2").split(","):
+                for bpc in os.environ.get("SWEEP_BPCS", "2,3").split(","):
+                    cases.append({"IKHIP_FABRIK_CORE": core, "IKHIP_FABRIK_BPC": bpc})
     for var in (() if cases else ("1", "2", "0")):
         for bpc in ("2", "4", "8"):
             for chunk in ("64", "256"):
