@@ -779,9 +779,11 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   // 64-point grabs beats 4 and 8 by 10-30 % (more lanes = fewer points per lane
   // = a longer divergent tail); 2 and 3 are within noise at 1-1.25M points, and
   // from 4M points on 3 wins by ~5 % at every tolerance (the tail matters less
-  // than the latency a third wave per SIMD hides).
+  // than the latency a third wave per SIMD hides), and so it does at 1M points
+  // with tol 1e-5 (56 iterations per point against 33 at 1e-3: 0.559 vs 0.586 ms
+  // per launch with the reuse iteration; at 1e-3 2 stays ahead, 0.386 vs 0.395).
   static const int bpc_env = env_int("IKHIP_FABRIK_BPC", 0);
-  const int bpc = bpc_env > 0 ? bpc_env : (n >= 2000000 ? 3 : 2);
+  const int bpc = bpc_env > 0 ? bpc_env : ((n >= 2000000 || tol < 1e-4) ? 3 : 2);
   static const int chunk = env_int("IKHIP_FABRIK_CHUNK", 64);
   a.chunk = chunk > 0 ? chunk : 64;
   unsigned pgrid = (unsigned)num_cus() * (unsigned)(bpc > 0 ? bpc : 8);
