@@ -221,13 +221,10 @@ struct FabArgs {
   int chunk;       // work-queue grab size of the persistent iteration kernel
   // hard-first ordering (see "Work order" below); unused when perm is null
   int32_t *perm;            // queue position -> point index
-  int32_t *iperm;           // point index -> queue position
-  uint8_t *status_in;       // ordered: the seed status by point (status is by position)
+  uint8_t *status_in;       // ordered: the seed status by point
   uint16_t *cell;           // per point: goal cell (bits 0-9) | cost class << 10
   FabOrderDev *ord;         // context-owned cost table and class histogram
   int nseg, seg_blocks;     // histogram segments, and blocks per segment
-  int32_t *iters_out;       // ordered: the caller's iterations (by point), nullable
-  double *joints_out;       // ordered: the caller's final joints (by point), nullable
   unsigned long long *dbg;  // diagnostic build only: iteration-kernel counters
 };
 
@@ -339,8 +336,17 @@ __device__ void order_scan(FabOrderDev *T, int nseg) {
   const int per = (E + 255) / 256, b0 = t * per, b1 = min(E, b0 + per);
   // scan position e = class (kOrdClasses-1 - e / nseg), segment e % nseg
   auto at = [&](int e) { return (kOrdClasses - 1 - e / nseg) * nseg + e % nseg; };
+  // the counts are read kScanBatch at a time with independent loads (a plain
+  // loop waits out one memory latency per entry: 15 us per call at 1M points)
+  constexpr int kScanBatch = 16;
   uint32_t s = 0;
-  for (int e = b0; e < b1; ++e) s += T->hist[at(e)];
+  for (int e0 = b0; e0 < b1; e0 += kScanBatch) {
+    uint32_t v[kScanBatch];
+#pragma unroll
+    for (int j = 0; j < kScanBatch; ++j) v[j] = (e0 + j < b1) ? T->hist[at(e0 + j)] : 0u;
+#pragma unroll
+    for (int j = 0; j < kScanBatch; ++j) s += v[j];
+  }
   part[t] = s;
   __syncthreads();
   for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan
@@ -350,11 +356,15 @@ __device__ void order_scan(FabOrderDev *T, int nseg) {
     __syncthreads();
   }
   uint32_t run = part[t] - s;
-  for (int e = b0; e < b1; ++e) {
-    const int k = at(e);
-    const uint32_t c = T->hist[k];
-    T->hist[k] = run;
-    run += c;
+  for (int e0 = b0; e0 < b1; e0 += kScanBatch) {
+    uint32_t v[kScanBatch];
+#pragma unroll
+    for (int j = 0; j < kScanBatch; ++j) v[j] = (e0 + j < b1) ? T->hist[at(e0 + j)] : 0u;
+#pragma unroll
+    for (int j = 0; j < kScanBatch; ++j) {
+      if (e0 + j < b1) T->hist[at(e0 + j)] = run;
+      run += v[j];
+    }
   }
 }
 
@@ -366,9 +376,17 @@ __device__ void order_fold(FabOrderDev *T) {
   for (int c = t; c < kOrdCells; c += 256) lm[c] = 0;
   __syncthreads();
   const unsigned int ns = T->nsample < kOrdMaxSample ? T->nsample : kOrdMaxSample;
-  for (unsigned int k = t; k < ns; k += 256) {
-    const unsigned int v = T->sample[k];
-    atomicMax(&lm[v >> 16], (v & 0xffffu) + 1u);
+  constexpr int kFoldBatch = 8;  // independent loads in flight (as in order_scan)
+  for (unsigned int k0 = t; k0 < ns; k0 += 256 * kFoldBatch) {
+    unsigned int v[kFoldBatch];
+#pragma unroll
+    for (int j = 0; j < kFoldBatch; ++j) {
+      const unsigned int k = k0 + 256u * j;
+      v[j] = k < ns ? T->sample[k] : 0xffffffffu;
+    }
+#pragma unroll
+    for (int j = 0; j < kFoldBatch; ++j)
+      if (v[j] != 0xffffffffu) atomicMax(&lm[v[j] >> 16], (v[j] & 0xffffu) + 1u);
   }
   __syncthreads();
   for (int c = t; c < kOrdCells; c += 256) {
@@ -448,7 +466,6 @@ __global__ __launch_bounds__(256) void fabrik_order_scatter_kernel(FabArgs a) {
     uint32_t pos = base[k] + rank;
     for (int v = 0; v < w; ++v) pos += wcnt[v][k];
     a.perm[pos] = (int32_t)i;
-    a.iperm[i] = (int32_t)pos;
   }
 }
 
@@ -457,8 +474,8 @@ __global__ __launch_bounds__(256) void fabrik_order_scatter_kernel(FabArgs a) {
 // IKHIP_FABRIK_CHUNK; small enough that every wave gets work at 1M points).
 
 // ORD: the queue is a.perm (work order above): a refilled lane gathers its
-// point's seed pose and goal, and writes its results at its queue position,
-// which the angles kernel maps back to the point.
+// point's seed pose and goal and keeps the point's index, where its results go
+// (so the angles kernel reads them in point order, coalesced).
 // CORE: 0 general sqrt / division, 1 sqrt_core / div_core, 2 the same with the
 // repeated distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
 template <int REFILL_MIN, bool ORD, int CORE>
@@ -473,6 +490,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   bool exhausted = false;
   bool active = false;
   int64_t idx = 0;  // queue position (= the point index unless ORD)
+  int64_t out = 0;  // the point index: where the lane's results go
   d3 J0 = {0, 0, 0}, J1 = J0, J2 = J0, J3 = J0, g = J0;
   double se = 1.0, ge = 1.0;
   int step = 0, st = IK_OK;
@@ -524,10 +542,12 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
           load_joints(a.seeds, p, Jn);
           g = {a.pts[3 * p], a.pts[3 * p + 1], a.pts[3 * p + 2]};
           st = a.status_in[p];
+          out = p;
         } else {
           load_joints(a.seeds, idx, Jn);
           g = {a.pts[3 * idx], a.pts[3 * idx + 1], a.pts[3 * idx + 2]};
           st = a.status[idx];
+          out = idx;
         }
         J0 = Jn[0]; J1 = Jn[1]; J2 = Jn[2]; J3 = Jn[3];
         if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
@@ -590,9 +610,9 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
         ++step;
       } else {
         d3 J[4] = {J0, J1, J2, J3};
-        store_joints(a.joints, idx, J);
-        a.iters[idx] = step;
-        a.status[idx] = (uint8_t)st;
+        store_joints(a.joints, out, J);
+        a.iters[out] = step;
+        a.status[out] = (uint8_t)st;
         active = false;
       }
     }
@@ -613,8 +633,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
 #undef IKHIP_DG
 }
 
-// 3. angles + stats (uniform work, one point per lane).  ORD: the iteration
-// results sit at queue positions (gathered through iperm); 1 in kOrdSample
+// 3. angles + stats (uniform work, one point per lane).  ORD: 1 in kOrdSample
 // points records (cell, iterations) for the next call's cost table.
 template <bool ORD>
 __global__ __launch_bounds__(256) void fabrik_angles_kernel(FabArgs a) {
@@ -622,20 +641,17 @@ __global__ __launch_bounds__(256) void fabrik_angles_kernel(FabArgs a) {
   bool valid = i < a.n;
   int it = 0;
   if (valid) {
-    const int64_t q = ORD ? (int64_t)a.iperm[i] : i;
-    int st = a.status[q];
-    it = a.iters[q];
+    int st = a.status[i];
+    it = a.iters[i];
     d3 J[4];
     double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
-    if (st == IK_OK || ORD) load_joints(a.joints, q, J);
+    if (st == IK_OK) load_joints(a.joints, i, J);
     if (st == IK_OK) get_angles(J, th, st);
     if (st != IK_OK) record_error(a.S, i, st);
     double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
     o[0] = make_double2(th[0], th[1]);
     o[1] = make_double2(th[2], th[3]);
     if constexpr (ORD) {
-      if (a.iters_out) a.iters_out[i] = it;
-      if (a.joints_out) store_joints(a.joints_out, i, J);
       if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
         a.ord->sample[i / kOrdSample] =
             ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) |
@@ -656,13 +672,13 @@ static size_t up256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t fabrik_scratch_bytes(int64_t n) {
   // seeds n*12 doubles, joints n*12 doubles, iters n int32, status n bytes;
-  // work order: perm + iperm n int32 each, cell n uint16, seed status n bytes
+  // work order: perm n int32, cell n uint16, seed status n bytes
   size_t b = 0;
   b += up256((size_t)n * 96);
   b += up256((size_t)n * 96);
   b += up256((size_t)n * 4);
   b += up256((size_t)n);
-  b += 2 * up256((size_t)n * 4) + up256((size_t)n * 2) + up256((size_t)n);
+  b += up256((size_t)n * 4) + up256((size_t)n * 2) + up256((size_t)n);
   return b + 1024;
 }
 
@@ -713,14 +729,11 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   a.S = S;
   a.chunk = 64;
   a.perm = nullptr;
-  a.iperm = nullptr;
   a.status_in = nullptr;
   a.cell = nullptr;
   a.ord = ord;
   a.nseg = 0;
   a.seg_blocks = 1;
-  a.iters_out = nullptr;
-  a.joints_out = nullptr;
   unsigned grid = (unsigned)((n + 255) / 256);
   if (variant == 0) {
     a.seeds = nullptr;
@@ -742,11 +755,10 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   static const int order_on = env_int("IKHIP_FABRIK_ORDER", 1);
   const bool ordered = ord && order_on && n < (int64_t)1 << 31;
   if (ordered) {
-    // iteration results land at queue positions in scratch; the angles kernel
-    // gathers them back to point order into the caller's (nullable) buffers
+    // the iteration kernel writes its results by point index (a lane keeps its
+    // point's index from the refill gather), straight into the caller's
+    // (nullable) iterations / joints buffers
     a.perm = reinterpret_cast<int32_t *>(p);
-    p += up256((size_t)n * 4);
-    a.iperm = reinterpret_cast<int32_t *>(p);
     p += up256((size_t)n * 4);
     a.cell = reinterpret_cast<uint16_t *>(p);
     p += up256((size_t)n * 2);
@@ -754,10 +766,8 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     a.seg_blocks = (int)((grid + kOrdMaxSeg - 1) / kOrdMaxSeg);
     if (a.seg_blocks < kOrdSegBlocksMin) a.seg_blocks = kOrdSegBlocksMin;
     a.nseg = (int)((grid + a.seg_blocks - 1) / a.seg_blocks);
-    a.iters_out = a.iters;
-    a.joints_out = a.joints;
-    a.iters = itmp;
-    a.joints = jtmp;
+    if (!a.joints) a.joints = jtmp;
+    if (!a.iters) a.iters = itmp;
     kt_begin("fabrik_seed_kernel", stream);
     hipLaunchKernelGGL(fabrik_seed_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
     kt_end(stream);
