@@ -539,16 +539,24 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
         d3 Jn[4];
         if constexpr (ORD) {
           const int64_t p = a.perm[idx];
+          st = a.status_in[p];
           load_joints(a.seeds, p, Jn);
           g = {a.pts[3 * p], a.pts[3 * p + 1], a.pts[3 * p + 2]};
-          st = a.status_in[p];
           out = p;
         } else {
+          st = a.status[idx];
           load_joints(a.seeds, idx, Jn);
           g = {a.pts[3 * idx], a.pts[3 * idx + 1], a.pts[3 * idx + 2]};
-          st = a.status[idx];
           out = idx;
         }
+        // consume the gathered operands here: left pending, their loads made the
+        // compiler put an s_waitcnt vmcnt(0) at the top of every step (the join
+        // of the refill and no-refill paths), which also waited out the result
+        // stores of the lanes that finished the step before
+        asm volatile("" ::"v"(st), "v"(Jn[0].x), "v"(Jn[0].y), "v"(Jn[0].z), "v"(Jn[1].x),
+                     "v"(Jn[1].y), "v"(Jn[1].z), "v"(Jn[2].x), "v"(Jn[2].y), "v"(Jn[2].z));
+        asm volatile("" ::"v"(Jn[3].x), "v"(Jn[3].y), "v"(Jn[3].z), "v"(g.x), "v"(g.y),
+                     "v"(g.z));
         J0 = Jn[0]; J1 = Jn[1]; J2 = Jn[2]; J3 = Jn[3];
         if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
         se = 1.0;
