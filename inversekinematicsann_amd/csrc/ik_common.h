@@ -257,18 +257,27 @@ __device__ __forceinline__ int seed_chain(const double *dh, const RobotConstDev 
   T1[11] = dh[4];
   ident4(T2);
   T2[3] = dh[8];
+  // the constants are read through the constant address space: wave-uniform
+  // s_load_dwordx* into SGPRs instead of 25 vector loads per lane, each a
+  // memory round trip on the seed's critical path (seed kernel VALU 28 % busy)
+  typedef const RobotConstDev __attribute__((address_space(4))) *RcConst;
+  const RcConst k = (RcConst)rc;
   ident4(X);
-  X[5] = rc->ca1; X[6] = -rc->sa1; X[9] = rc->sa1; X[10] = rc->ca1;
+  const double ca1 = k->ca1, sa1 = k->sa1;
+  X[5] = ca1; X[6] = -sa1; X[9] = sa1; X[10] = ca1;
   mm4_r3(R, T1, M);
   mm4_r3(M, T2, M);
   mm4_r3(M, X, M);
   J[0].x = M[3]; J[0].y = M[7]; J[0].z = M[11];
 #pragma unroll
   for (int i = 1; i < 4; ++i) {
-    mm4_r3(M, rc->A[i - 1], M);
+    double A[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) A[e] = k->A[i - 1][e];
+    mm4_r3(M, A, M);
     J[i].x = M[3]; J[i].y = M[7]; J[i].z = M[11];
   }
-  return rc->st;
+  return k->st;
 }
 
 // Same chain, writing all four cumulative transforms (row-major 4x4 each).
