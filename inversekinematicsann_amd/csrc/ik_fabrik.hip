@@ -13,6 +13,7 @@
 //    lane) -> angles_kernel (law of cosines + per-batch stats).
 //  * simple: everything in one kernel, one point per lane, no refill.
 // Per point the state is 4 joints + goal (15 doubles) held in VGPRs.
+#include <atomic>
 #include <cmath>
 
 #include "ik_common.h"
@@ -690,16 +691,21 @@ size_t fabrik_scratch_bytes(int64_t n) {
   return b + 1024;
 }
 
-static int g_cus = 0;
+// CUs of the current device, cached per device index (relaxed atomics: every
+// writer stores the same value)
 static int num_cus() {
-  if (g_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        g_cus <= 0)
-      g_cus = 256;
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::atomic<int> *slot = (dev >= 0 && dev < 64) ? &cache[dev] : nullptr;
+  int v = slot ? slot->load(std::memory_order_relaxed) : 0;
+  if (v <= 0) {
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    if (slot) slot->store(v, std::memory_order_relaxed);
   }
-  return g_cus;
+  return v;
 }
 
 template <int REFILL_MIN, bool ORD>
