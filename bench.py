@@ -17,6 +17,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import math
 import json
 import os
 import sys
@@ -43,7 +44,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--method", choices=["ann", "fabrik"], default="ann")
+    ap.add_argument("--method", choices=["ann", "fabrik", "fk"], default="ann",
+                    help="fk: the batched FK kernel alone (profiling; no secondaries)")
     ap.add_argument("--points", type=int, default=1_000_000, help="points per GPU")
     ap.add_argument("--tol", type=float, default=1e-3)
     ap.add_argument("--max-iter", type=int, default=100)
@@ -266,6 +268,41 @@ def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
     return res
 
 
+FK_BYTES_PER_POINT = 32 + 24   # float64 angles in, float64 effector xyz out
+
+
+def run_fk(ctx, dpts, n, args, world):
+    """Batched FK (forward.py:73-94, the DH chain) on n angle
+    vectors drawn uniformly in [-pi, pi): its bound is HBM (56 B per point) or
+    the float64 sin/cos + products, whichever is longer."""
+    import torch
+    from inversekinematicsann_amd import _native
+    g = torch.Generator(device="cuda")
+    g.manual_seed(7)
+    dang = (torch.rand((n, 4), generator=g, dtype=torch.float64, device="cuda") * 2 - 1) * math.pi
+    dxyz = torch.empty((n, 3), dtype=torch.float64, device="cuda")
+    flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
+
+    def step():
+        ctx.fk_device(dang, dxyz, flags=flags)
+
+    res = timed(ctx, step, args, world)
+    res["outputs"] = {"xyz": dxyz}
+    k = res["kernels"].get("fk_kernel")
+    achieved = FK_BYTES_PER_POINT * n / (k / 1e3) if k else None
+    res["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None,
+                       "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                       "frac": achieved / HBM_PEAK if achieved else None,
+                       "traffic": load_traffic(args.traffic_file, "fk_kernel"),
+                       "kernel": "fk_kernel", "kernel_ms": k,
+                       "algorithmic_bytes_per_point": FK_BYTES_PER_POINT,
+                       "points_per_launch": n}
+    res["dtype"] = "f64"
+    res["unit"] = "FK evaluations/s"
+    res["workload"] = f"FK (DH chain, float64), {_pts(n)} angle vectors per GPU"
+    return res
+
+
 def timed(ctx, step, args, world):
     import torch
     for _ in range(args.warmup):
@@ -439,20 +476,22 @@ def main():
     other_modes = [m for m in ("fp32", "bf16x6", "fp16x3") if m != args.ann_mode]
     runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik,
                # configs[4]'s divergent-iteration stress settings on the per-GPU batch
-               "fabrik_tol1e-5": lambda *a: run_fabrik(*a, tol=1e-5, max_iter=200)}
+               "fabrik_tol1e-5": lambda *a: run_fabrik(*a, tol=1e-5, max_iter=200),
+               "fk": run_fk}
     for om in other_modes:
         runners[f"ann_{om}"] = (lambda mm: lambda *a: run_ann(*a, mode=mm))(om)
     res = runners[args.method](ctx, dpts, n, args, world)
     outputs = {args.method: res["outputs"]}
     secondary = {}
-    if args.secondary:
-        others = (["fabrik", "fabrik_tol1e-5"] + [f"ann_{om}" for om in other_modes]
-                  if args.method == "ann" else ["ann", "fabrik_tol1e-5"])
+    if args.secondary and args.method != "fk":
+        others = (["fabrik", "fabrik_tol1e-5"] + [f"ann_{om}" for om in other_modes] + ["fk"]
+                  if args.method == "ann" else ["ann", "fabrik_tol1e-5", "fk"])
         if args.method == "fabrik" and (args.tol, args.max_iter) == (1e-5, 200):
             others.remove("fabrik_tol1e-5")
         for other in others:
             r2 = runners[other](ctx, dpts, n, args, world)
             secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
+                                "unit": r2.get("unit", "IK solutions/s"),
                                 "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
                                 "roofline": r2["roofline"], "workload": r2["workload"],
                                 **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
@@ -462,7 +501,7 @@ def main():
     total = n * world
     value = total / (res["ms_per_step"] / 1e3)
     line = {
-        "metric": METRIC, "value": value, "unit": "IK solutions/s", "n_gpus": world,
+        "metric": METRIC, "value": value, "unit": res.get("unit", "IK solutions/s"), "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": res["dtype"],
@@ -484,7 +523,7 @@ def main():
             line[k] = res[k]
     if secondary:
         line["secondary"] = secondary
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and args.method != "fk":
         def host(o):
             return {k: v[:max(CPU_SAMPLE.values())].cpu().numpy() for k, v in o.items()}
         line["cpu_baseline"] = cpu_baseline(args.method, args, pts, host(outputs[args.method]))

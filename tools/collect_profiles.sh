@@ -7,7 +7,7 @@ R=${1:?round name}
 OUT=gpurun_out
 DST=profiles/$R
 mkdir -p $DST/pmc
-for m in ann fabrik ann_bf16x6 ann_fp16x3; do
+for m in ann fabrik ann_bf16x6 ann_fp16x3 fk; do
   # gpurun_out/ accumulates the runs of earlier calls: take the newest
   cp "$(ls -t $OUT/prof_stats_$m/*/*_kernel_stats.csv | head -1)" $DST/${m}_kernel_stats.csv
   for c in fetch write; do

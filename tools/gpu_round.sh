@@ -20,7 +20,9 @@ fi
 step bench_ann 600 python bench.py --steps ${STEPS:-10} --warmup 2 --cpu-seconds ${CPUS:-10}
 cp $OUT/bench_ann.log $OUT/bench_ann.json
 if [ "${PROFILE:-1}" = "1" ]; then
-  for m in ann fabrik ann_bf16x6 ann_fp16x3; do
+  # MODES: a subset to re-profile; the traffic of the others is kept from profiles/
+  [ -f $OUT/traffic.json ] || cp profiles/traffic.json $OUT/traffic.json
+  for m in ${MODES:-ann fabrik ann_bf16x6 ann_fp16x3 fk}; do
     case $m in
       ann_bf16x6) BARGS="--method ann --ann-mode bf16x6" ;;
       ann_fp16x3) BARGS="--method ann --ann-mode fp16x3" ;;
