@@ -48,83 +48,144 @@ void launch_check_limits(const RobotDev &r, const double *pts, int64_t n, DevSta
   kt_end(st);
 }
 
-// The translations of M_1..M_4 from the closed form of each DH matrix,
+// The effector from the closed form of each DH matrix,
 // A_k = [[c, -s ca, s sa, a c], [s, c ca, -c sa, a s], [0, sa, ca, d]] (row 3 is
 // [0, 0, 0, 1]), with cos / sin(alpha_k) per robot (host, launch_fk).  Every
 // entry is the single product the reference's ((Rz Tz) Tx) Rx chain reduces to
-// (its other terms multiply exact zeros and ones), so A_k and the cumulative
-// rows-0..2 products (mm4_r3: the reference's k-ordered FMA chains) agree with
-// fk_chain to the last bits up to the cos / sin(alpha) rounding: three 4x4
-// products and two cos / sin pairs fewer per joint.
+// (its other terms multiply exact zeros and ones), so A_k agrees with fk_chain's
+// up to the cos / sin(alpha) rounding and signed zeros: three 4x4 products and
+// two cos / sin pairs fewer per joint.  cos / sin(theta) come from sincos_fk
+// (|error| <= 1.2e-16; the positions stay within 1e-15 of fk_chain's).
 struct FkConst {
   double ca[4], sa[4];
 };
 
-__device__ __forceinline__ int fk_chain_closed(const double *dh, const FkConst &k,
-                                               const double th[4], d3 J[4]) {
+// The effector of the chain from the closed-form A_k: rows 0-2 of the cumulative
+// products, each element the reference's k-ordered FMA chain with the terms that
+// multiply A_k's exact zeros dropped (they add a signed zero to a finite sum) and
+// its exact one kept as the add it is; the last product forms column 3 only.
+__device__ __forceinline__ int fk_effector(const double *dh, const FkConst &k,
+                                           const double th[4], d3 &E) {
   int st = IK_OK;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
     if (!angle_ok(th[i]) || !angle_ok(dh[12 + i])) st = IK_E_ANGLE_RANGE;
-  double M[12], A[16];
+  double M[12];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     double s, c;
-    sincos(th[i], &s, &c);
+    sincos_fk(th[i], &s, &c);
     const double ca = k.ca[i], sa = k.sa[i], a = dh[8 + i], d = dh[4 + i];
-    A[0] = c;   A[1] = -s * ca; A[2] = s * sa;  A[3] = a * c;
-    A[4] = s;   A[5] = c * ca;  A[6] = -c * sa; A[7] = a * s;
-    A[8] = 0.0; A[9] = sa;      A[10] = ca;     A[11] = d;
-    A[12] = 0.0; A[13] = 0.0;   A[14] = 0.0;    A[15] = 1.0;
+    // A_k rows 0-2: [[c, -s ca, s sa, a c], [s, c ca, -c sa, a s], [0, sa, ca, d]]
+    const double A00 = c, A01 = -s * ca, A02 = s * sa, A03 = a * c;
+    const double A10 = s, A11 = c * ca, A12 = -c * sa, A13 = a * s;
+    const double A21 = sa, A22 = ca, A23 = d;
     if (i == 0) {
-#pragma unroll
-      for (int e = 0; e < 12; ++e) M[e] = A[e];
+      M[0] = A00; M[1] = A01; M[2] = A02;  M[3] = A03;
+      M[4] = A10; M[5] = A11; M[6] = A12;  M[7] = A13;
+      M[8] = 0.0; M[9] = A21; M[10] = A22; M[11] = A23;
     } else {
-      mm4_r3(M, A, M);
+      double T[12];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double m0 = M[4 * r], m1 = M[4 * r + 1], m2 = M[4 * r + 2], m3 = M[4 * r + 3];
+        T[4 * r + 3] = __builtin_fma(m2, A23, __builtin_fma(m1, A13, m0 * A03)) + m3;
+        if (i < 3) {
+          T[4 * r] = __builtin_fma(m1, A10, m0 * A00);
+          T[4 * r + 1] = __builtin_fma(m2, A21, __builtin_fma(m1, A11, m0 * A01));
+          T[4 * r + 2] = __builtin_fma(m2, A22, __builtin_fma(m1, A12, m0 * A02));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 12; ++e) M[e] = T[e];
     }
-    J[i].x = M[3]; J[i].y = M[7]; J[i].z = M[11];
   }
+  E = {M[3], M[7], M[11]};
   return st;
 }
 
 // mats (nullable): the four cumulative 4x4 transforms M_1..M_4 of each point,
-// the second return value of fkine (forward.py:94).
-__global__ __launch_bounds__(256) void fk_kernel(RobotDev r, FkConst kc,
-                                                  const double *__restrict__ ang,
-                                                  int64_t n, double *__restrict__ xyz,
-                                                  double *__restrict__ mats, DevStats *S) {
+// the second return value of fkine (forward.py:94), through fk_chain_mats.
+__global__ __launch_bounds__(256) void fk_mats_kernel(RobotDev r, const double *__restrict__ ang,
+                                                       int64_t n, double *__restrict__ xyz,
+                                                       double *__restrict__ mats, DevStats *S) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   double th[4] = {ang[4 * i], ang[4 * i + 1], ang[4 * i + 2], ang[4 * i + 3]};
-  d3 J[4];
-  int st;
-  if (mats) {
-    double *o = mats + 64 * i;
-    st = fk_chain_mats(r.dh, th, o);
-    for (int k = 0; k < 4; ++k) J[k] = {o[16 * k + 3], o[16 * k + 7], o[16 * k + 11]};
-  } else {
-    st = fk_chain_closed(r.dh, kc, th, J);
-  }
+  double *o = mats + 64 * i;
+  const int st = fk_chain_mats(r.dh, th, o);
+  d3 e = {o[51], o[55], o[59]};
   if (st != IK_OK) {
     record_error(S, i, st);
-    J[3].x = J[3].y = J[3].z = __builtin_nan("");
+    e.x = e.y = e.z = __builtin_nan("");
   }
-  xyz[3 * i] = J[3].x;
-  xyz[3 * i + 1] = J[3].y;
-  xyz[3 * i + 2] = J[3].z;
+  xyz[3 * i] = e.x;
+  xyz[3 * i + 1] = e.y;
+  xyz[3 * i + 2] = e.z;
+}
+
+// The effector only: a grid-stride loop over the points whose next angles are
+// loaded before the current point's chain runs, so the HBM round trip of one
+// point hides under the arithmetic of the one before (one point per lane and
+// launch left most of the kernel waiting on its loads at 4 waves per SIMD).
+__global__ __launch_bounds__(256) void fk_kernel(RobotDev r, FkConst kc,
+                                                  const double *__restrict__ ang,
+                                                  int64_t n, double *__restrict__ xyz,
+                                                  DevStats *S) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double2 *a2 = reinterpret_cast<const double2 *>(ang);
+  double2 p0 = a2[2 * i], p1 = a2[2 * i + 1];
+  for (; i < n; i += stride) {
+    const double th[4] = {p0.x, p0.y, p1.x, p1.y};
+    const int64_t nx = i + stride;
+    if (nx < n) {
+      p0 = a2[2 * nx];
+      p1 = a2[2 * nx + 1];
+    }
+    d3 e;
+    const int st = fk_effector(r.dh, kc, th, e);
+    if (st != IK_OK) {
+      record_error(S, i, st);
+      e.x = e.y = e.z = __builtin_nan("");
+    }
+    xyz[3 * i] = e.x;
+    xyz[3 * i + 1] = e.y;
+    xyz[3 * i + 2] = e.z;
+  }
+}
+
+static int fk_cus() {
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  return cus;
 }
 
 void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, double *joints,
                DevStats *S, hipStream_t st) {
   if (n <= 0) return;
-  unsigned grid = (unsigned)((n + 255) / 256);
-  FkConst kc;
-  for (int i = 0; i < 4; ++i) {
-    kc.ca[i] = std::cos(r.dh[12 + i]);
-    kc.sa[i] = std::sin(r.dh[12 + i]);
-  }
+  const unsigned grid_all = (unsigned)((n + 255) / 256);
   kt_begin("fk_kernel", st);
-  hipLaunchKernelGGL(fk_kernel, dim3(grid), dim3(256), 0, st, r, kc, ang, n, xyz, joints, S);
+  if (joints) {
+    hipLaunchKernelGGL(fk_mats_kernel, dim3(grid_all), dim3(256), 0, st, r, ang, n, xyz,
+                       joints, S);
+  } else {
+    FkConst kc;
+    for (int i = 0; i < 4; ++i) {
+      kc.ca[i] = std::cos(r.dh[12 + i]);
+      kc.sa[i] = std::sin(r.dh[12 + i]);
+    }
+    // resident blocks only (8 per CU): every lane walks several points
+    // (2, 4, 6, 8 blocks per CU or one point per lane all measured 17.0-17.3 us per
+    // 1M points: at that size the launch's fixed cost, ~6 us, is a third of it)
+    const unsigned cap = (unsigned)fk_cus() * 8;
+    const unsigned grid = grid_all < cap ? grid_all : cap;
+    hipLaunchKernelGGL(fk_kernel, dim3(grid), dim3(256), 0, st, r, kc, ang, n, xyz, S);
+  }
   kt_end(st);
 }
 

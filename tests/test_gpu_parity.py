@@ -393,3 +393,36 @@ def test_fabrik_custom_links_match_oracle(links):
             assert (st.first_err, st.first_err_code) == want
     finally:
         c.close()
+
+
+def test_fk_full_angle_range_vs_oracle():
+    """The FK kernel's closed-form DH matrices and range-limited sincos over the
+    whole legal angle range [-2 pi, 2 pi] (forward.py:23-25), its edges, and a few
+    out-of-range angles (IK_E_ANGLE_RANGE at the first one): effector positions
+    within 1e-12 of the oracle's DH-product restatement, with a custom DH table too."""
+    rng = np.random.default_rng(31)
+    ang = rng.uniform(-2 * math.pi, 2 * math.pi, size=(200_000, 4))
+    ang[:8] = [[2 * math.pi] * 4, [-2 * math.pi] * 4, [0.0] * 4, [math.pi / 2] * 4,
+               [-math.pi / 2] * 4, [math.pi] * 4, [1e-300, -1e-300, 5e-324, 0.0],
+               [math.pi / 4, 3 * math.pi / 4, -3 * math.pi / 4, 7 * math.pi / 4]]
+    from inversekinematicsann_amd import _native
+    c = _native.Context(0)
+    for dh in (O.DH, np.array([[0.3, -1.1, 0.2, 0.0], [1.5, 0.25, 0.0, -0.5],
+                               [0.0, 1.7, 2.3, 0.9], [math.pi / 2, -0.4, 0.0, 1.2]])):
+        c.set_robot(dh, O.LINKS, O.LIMITS)
+        xyz, _, st = c.fk(ang)
+        rxyz, _, rst = O.fk(ang, dh=dh)
+        assert st.first_err == -1 and not rst.any()
+        assert np.abs(xyz - rxyz).max() <= 1e-12
+    c.set_robot(O.DH, O.LINKS, O.LIMITS)
+    bad = ang[:100].copy()
+    bad[37, 2] = 2 * math.pi + 1e-9
+    bad[60, 0] = -7.0
+    xyz, _, st = c.fk(bad)
+    assert (st.first_err, st.first_err_code) == (37, 4)
+    assert np.isnan(xyz[37]).all() and np.isnan(xyz[60]).all()
+    rxyz, _, _ = O.fk(bad)
+    ok = np.ones(100, bool)
+    ok[[37, 60]] = False
+    assert np.abs(xyz[ok] - rxyz[ok]).max() <= 1e-12
+    c.close()
