@@ -807,7 +807,10 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   // with tol 1e-5 (56 iterations per point against 33 at 1e-3: 0.559 vs 0.586 ms
   // per launch with the reuse iteration; at 1e-3 2 stays ahead, 0.386 vs 0.395).
   static const int bpc_env = env_int("IKHIP_FABRIK_BPC", 0);
-  const int bpc = bpc_env > 0 ? bpc_env : ((n >= 2000000 || tol < 1e-4) ? 3 : 2);
+  // (4M / 10M points at tol 1e-3: 4 per CU is 2 % ahead of 3; at 1e-5 they are even)
+  const int bpc = bpc_env > 0 ? bpc_env
+                              : (n >= 4000000 && tol >= 1e-4) ? 4
+                                                              : ((n >= 2000000 || tol < 1e-4) ? 3 : 2);
   static const int chunk = env_int("IKHIP_FABRIK_CHUNK", 64);
   a.chunk = chunk > 0 ? chunk : 64;
   unsigned pgrid = (unsigned)num_cus() * (unsigned)(bpc > 0 ? bpc : 8);
