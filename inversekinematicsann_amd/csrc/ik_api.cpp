@@ -81,6 +81,7 @@ struct ik_ctx {
   float ann_hinv[kAnnMaxLayers] = {};      // fp16x3: 2^-(weight pre-scale exponent)
   int ann_mode = IK_ANN_FP32;
   int fabrik_variant = 1;
+  int fabrik_bpc = 0;   // IKHIP_FABRIK_BPC: iteration-kernel blocks per CU (0 = size rule)
   int fabrik_core = 2;  // IKHIP_FABRIK_CORE: 2 core + reuse, 1 sqrt_core / div_core, 0 general
   KTimer kt;
   unsigned long long *dbg = nullptr;  // diagnostic stamp buffer (ik_ctx_set_debug)
@@ -211,6 +212,7 @@ int ik_ctx_create(int device, ik_ctx **out) {
   }
   if (const char *v = std::getenv("IKHIP_FABRIK_VARIANT")) c->fabrik_variant = std::atoi(v);
   if (const char *v = std::getenv("IKHIP_FABRIK_CORE")) c->fabrik_core = std::atoi(v);
+  if (const char *v = std::getenv("IKHIP_FABRIK_BPC")) c->fabrik_bpc = std::atoi(v);
   if (const char *v = std::getenv("IKHIP_ANN_MODE"))
     c->ann_mode = std::strcmp(v, "bf16x6") == 0   ? IK_ANN_BF16X6
                   : std::strcmp(v, "fp16x3") == 0 ? IK_ANN_FP16X3
@@ -425,7 +427,7 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
   launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj,
                       !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
                       c->fabrik_variant, c->fabrik_core, c->fab_ord, c->rconst,
-                      c->dbg);
+                      c->dbg, c->fabrik_bpc);
   IK_HIP(hipGetLastError());
   if (!dev && n > 0) {
     IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));

@@ -436,7 +436,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t st,
                          int variant, int core, FabOrderDev *ord, const RobotConstDev *rc,
-                         unsigned long long *dbg);
+                         unsigned long long *dbg, int bpc = 0);
 constexpr size_t kFabrikDebugWords = 64 + 4 * 4000;  // diagnostic build counters
 // Per-robot seed constants (RobotConstDev) into device memory, on stream st.
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t st);

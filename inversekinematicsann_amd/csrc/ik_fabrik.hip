@@ -725,7 +725,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
                          int variant, int core_req, FabOrderDev *ord,
-                         const RobotConstDev *rc, unsigned long long *dbg) {
+                         const RobotConstDev *rc, unsigned long long *dbg, int bpc_req) {
   if (n <= 0) return;
   FabArgs a;
   a.r = r;
@@ -806,9 +806,9 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   // than the latency a third wave per SIMD hides), and so it does at 1M points
   // with tol 1e-5 (56 iterations per point against 33 at 1e-3: 0.559 vs 0.586 ms
   // per launch with the reuse iteration; at 1e-3 2 stays ahead, 0.386 vs 0.395).
-  static const int bpc_env = env_int("IKHIP_FABRIK_BPC", 0);
   // (4M / 10M points at tol 1e-3: 4 per CU is 2 % ahead of 3; at 1e-5 they are even)
-  const int bpc = bpc_env > 0 ? bpc_env
+  // bpc_req: the context's IKHIP_FABRIK_BPC (0 = this rule)
+  const int bpc = bpc_req > 0 ? bpc_req
                               : (n >= 4000000 && tol >= 1e-4) ? 4
                                                               : ((n >= 2000000 || tol < 1e-4) ? 3 : 2);
   static const int chunk = env_int("IKHIP_FABRIK_CHUNK", 64);

@@ -111,3 +111,34 @@ def test_ann_full_size(ctx, mode):
     assert np.abs(err - e).max() <= 1e-9
     assert st.max_fk_err == pytest.approx(float(err.max()), rel=1e-15)
     assert st.sum_fk_err == pytest.approx(float(err.sum()), rel=1e-9)
+
+
+@pytest.mark.gpu
+def test_fabrik_results_independent_of_grid():
+    """4M points at tol 1e-3 run on 4 blocks per CU by default; the persistent
+    grid only changes which lane solves which point, so angles and iteration
+    counts are bit-identical to a 2-blocks-per-CU run, and a head slice matches
+    the oracle."""
+    import os
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    from oracle import oracle as O
+    pts = random_dist(4_000_000, seed=41)
+    out = {}
+    for bpc in ("", "2"):
+        if bpc:
+            os.environ["IKHIP_FABRIK_BPC"] = bpc
+        try:
+            c = _native.Context(0)
+        finally:
+            os.environ.pop("IKHIP_FABRIK_BPC", None)
+        try:
+            out[bpc] = c.fabrik_solve(pts, 1e-3, 100)[:2]
+        finally:
+            c.close()
+    (a4, i4), (a2, i2) = out[""], out["2"]
+    assert np.array_equal(i4, i2)
+    assert np.array_equal(a4.view(np.uint64), a2.view(np.uint64))
+    rang, rit, _, _ = O.fabrik_ikine(pts[:4096], 1e-3, 100)
+    assert np.array_equal(i4[:4096], rit)
+    assert np.abs(a4[:4096] - rang).max() <= 1e-9
