@@ -48,6 +48,11 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "bpc":  # grid size across tolerances / sizes
         for bpc in ("2", "3", "4"):
             cases.append({"IKHIP_FABRIK_BPC": bpc})
+    if len(sys.argv) > 1 and sys.argv[1] == "chunk":  # grab size x grid, twice
+        for _rep in range(2):
+            for ch in os.environ.get("SWEEP_CHUNKS", "64,96,128,192").split(","):
+                for bpc in os.environ.get("SWEEP_BPCS", "2,3").split(","):
+                    cases.append({"IKHIP_FABRIK_CHUNK": ch, "IKHIP_FABRIK_BPC": bpc})
     if len(sys.argv) > 1 and sys.argv[1] == "core":  # iteration sequences x grid, twice
         for _rep in range(2):
             for core in os.environ.get("SWEEP_CORES", "1,2").split(","):
