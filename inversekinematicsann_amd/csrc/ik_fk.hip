@@ -135,14 +135,16 @@ __global__ __launch_bounds__(256) void fk_kernel(RobotDev r, FkConst kc,
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const double2 *a2 = reinterpret_cast<const double2 *>(ang);
-  double2 p0 = a2[2 * i], p1 = a2[2 * i + 1];
+  // (8-byte loads: a caller's device pointer need not be 16-byte aligned)
+  double p0 = ang[4 * i], p1 = ang[4 * i + 1], p2 = ang[4 * i + 2], p3 = ang[4 * i + 3];
   for (; i < n; i += stride) {
-    const double th[4] = {p0.x, p0.y, p1.x, p1.y};
+    const double th[4] = {p0, p1, p2, p3};
     const int64_t nx = i + stride;
     if (nx < n) {
-      p0 = a2[2 * nx];
-      p1 = a2[2 * nx + 1];
+      p0 = ang[4 * nx];
+      p1 = ang[4 * nx + 1];
+      p2 = ang[4 * nx + 2];
+      p3 = ang[4 * nx + 3];
     }
     d3 e;
     const int st = fk_effector(r.dh, kc, th, e);
