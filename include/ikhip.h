@@ -94,7 +94,8 @@ int ik_fk(ik_ctx *ctx, const double *ang, int64_t n, double *xyz, double *mats, 
  * FabrikInverseKinematics.ikine, kinematics/inverse.py:115-139 (+ check_limits,
  * Fabrik.calculate fabrik.py:44-67, __get_angles inverse.py:54-112), batched:
  * pts n x 3 -> ang n x 4 (float64), iters n (nullable), final joint positions
- * n x 4 x 3 (nullable).  tol/max_iter: Fabrik(err_margin, max_iter_num). */
+ * n x 4 x 3 (nullable).  tol/max_iter: Fabrik(err_margin, max_iter_num).
+ * With IK_F_DEVICE, ang must be 16-byte aligned (else IK_E_BADARG). */
 int ik_fabrik_solve(ik_ctx *ctx, const double *pts, int64_t n, double tol, int32_t max_iter,
                     double *ang, int32_t *iters, double *joints, int flags, ik_stats *stats);
 
@@ -119,7 +120,8 @@ int ik_ann_load(ik_ctx *ctx, int n_layers, const int32_t *dims, const int32_t *a
 /* ANN.predict, kinematics/ann.py:70-76 (+ check_limits for AnnInverseKinematics.ikine,
  * inverse.py:152-155 unless IK_F_NO_LIMITS): pts n x 3 float64 -> ang n x 4
  * float32.  fk_err (nullable) n float64: |FK(ang) - p|_2, the cli.py:54-61
- * round trip, fused into the same launch; its max/sum go to stats. */
+ * round trip, fused into the same launch; its max/sum go to stats.  With
+ * IK_F_DEVICE, ang must be 16-byte aligned (else IK_E_BADARG). */
 int ik_ann_solve(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *fk_err,
                  int flags, ik_stats *stats);
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -397,6 +398,8 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
     return fail(IK_E_BADARG, "ik_fabrik_solve: bad args");
   if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
     return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  if ((flags & IK_F_DEVICE) && (reinterpret_cast<uintptr_t>(ang) & 15))
+    return fail(IK_E_BADARG, "ik_fabrik_solve: device ang must be 16-byte aligned");
   int rc = set_dev(c);
   if (rc) return rc;
   KtScope kts(c);
@@ -597,6 +600,8 @@ int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk
   if (!c->ann_loaded) return fail(IK_E_NOMODEL, "ik_ann_solve: no model loaded (ik_ann_load)");
   if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
     return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  if ((flags & IK_F_DEVICE) && (reinterpret_cast<uintptr_t>(ang) & 15))
+    return fail(IK_E_BADARG, "ik_ann_solve: device ang must be 16-byte aligned");
   int rc = set_dev(c);
   if (rc) return rc;
   KtScope kts(c);

@@ -45,6 +45,14 @@ def test_bad_arguments_are_refused(ctx):
     rc, msg = _rc_msg(ctx, L.ik_fabrik_solve(h, pts.ctypes.data, 4, 1e-3, 100, ang.ctypes.data,
                                              None, None, N.IK_F_ASYNC, ctypes.byref(st)))
     assert rc == N.IK_E_BADARG and "IK_F_ASYNC" in msg
+    # device outputs the kernels store 16 bytes at a time must be 16-byte aligned
+    import torch
+    dp = torch.zeros((4, 3), dtype=torch.float64, device="cuda")
+    da = torch.zeros(17, dtype=torch.float64, device="cuda")
+    rc, msg = _rc_msg(ctx, L.ik_fabrik_solve(h, dp.data_ptr(), 4, 1e-3, 100,
+                                             da.data_ptr() + 8, None, None, N.IK_F_DEVICE,
+                                             ctypes.byref(st)))
+    assert rc == N.IK_E_BADARG and "aligned" in msg
     # generic chains: 2..8 joints only
     with pytest.raises(N.NativeError) as ei:
         ctx.fabrik_calc(np.ones(9), np.zeros((9, 3)), np.zeros((2, 3)))
