@@ -81,13 +81,14 @@ def test_fabrik_full_size(ctx, n, tol, max_iter, seed):
     assert np.array_equal(ang2.view(np.uint64), ang.view(np.uint64))
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16x6", "fp16x3"])
-def test_ann_full_size(ctx, mode):
-    """configs[1]: the reference architecture on 1M random_dist points."""
+@pytest.mark.parametrize("mode,n", [("fp32", 1_000_000), ("bf16x6", 1_000_000),
+                                    ("fp16x3", 1_000_000), ("fp32", 10_000_000)])
+def test_ann_full_size(ctx, mode, n):
+    """configs[1]: the reference architecture on 1M random_dist points (and
+    configs[3]'s whole 10M-point batch on one GPU in fp32)."""
     from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER as XS, \
         REFERENCE_Y_SCALER as YS
     from inversekinematicsann_amd.robot.position_generator import random_dist
-    n = 1_000_000
     m = glorot_model(dims=(3,) + (500,) * 12 + (4,), seed=0)
     ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
     pts = random_dist(n, seed=0)
