@@ -232,18 +232,25 @@ def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
     from inversekinematicsann_amd import _native
     dang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
     dit = torch.empty(n, dtype=torch.int32, device="cuda")
+    derr = torch.empty(n, dtype=torch.float64, device="cuda")
     flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
 
     gather = make_gather(dang, args, world)
 
     def step():
-        ctx.fabrik_solve_device(dpts, dang, dit, None, tol, max_iter, flags=flags)
+        # the --verbose FK round trip (cli.py:54-72) in the same launch as the angles
+        ctx.fabrik_solve_device(dpts, dang, dit, None, tol, max_iter, flags=flags, fk_err=derr)
         gather()
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
     res["mean_iters"] = st.sum_iters / n
     res["n_capped"] = st.n_capped
+    res["max_fk_err"] = max_over_ranks(st.max_fk_err, world)
+    res["mean_fk_err"] = sum_over_ranks(st.sum_fk_err, world) / (n * world)
+    fin = derr[:1 << 24]
+    res["p99_fk_err"] = max_over_ranks(float(torch.quantile(fin[torch.isfinite(fin)], 0.99)),
+                                       world)
     res["outputs"] = {"ang": dang, "iters": dit}
     res["end_to_end"] = end_to_end(
         lambda hp: ctx.fabrik_solve(hp, tol, max_iter), dpts, args, world)
@@ -263,7 +270,8 @@ def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
                                                        "fabrik_diag_summary.json"),
                                           "fabrik_iter_kernel")}
     res["dtype"] = "f64"
-    res["workload"] = (f"FABRIK ikine (seed FK + loop + angles), tol {tol:g} / "
+    res["workload"] = (f"FABRIK ikine (seed FK + loop + angles) + fused FK round-trip error, "
+                       f"tol {tol:g} / "
                        f"{max_iter} iterations, float64, {_pts(n)} random_dist points per GPU")
     return res
 

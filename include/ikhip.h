@@ -99,6 +99,15 @@ int ik_fk(ik_ctx *ctx, const double *ang, int64_t n, double *xyz, double *mats, 
 int ik_fabrik_solve(ik_ctx *ctx, const double *pts, int64_t n, double tol, int32_t max_iter,
                     double *ang, int32_t *iters, double *joints, int flags, ik_stats *stats);
 
+/* ik_fabrik_solve plus the --verbose round trip of the reference CLI
+ * (cli.py:54-72, IkineCommand, the base of both --method commands): fk_err
+ * (nullable) n float64 |FK(ang) - p|_2, computed in the same launch as the
+ * angles; its max/sum over the finite values go to stats (max_fk_err,
+ * sum_fk_err).  A point whose solve raised has fk_err NaN. */
+int ik_fabrik_solve_fk(ik_ctx *ctx, const double *pts, int64_t n, double tol, int32_t max_iter,
+                       double *ang, int32_t *iters, double *joints, double *fk_err, int flags,
+                       ik_stats *stats);
+
 /* Fabrik.calculate, kinematics/fabrik.py:44-67, batched over n goals for a chain
  * of nj (2..8) joints: init is n x nj x 3 (or nj x 3 shared by all goals when
  * init_shared != 0), goals n x 3 -> joints n x nj x 3, iters n (nullable). */

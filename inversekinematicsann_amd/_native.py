@@ -28,7 +28,7 @@ ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
 
 EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_ctx_get_stream",
                     "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk",
-                    "ik_fabrik_solve", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
+                    "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode")
 ANN_MODES = {"fp32": 0, "bf16x6": 1, "fp16x3": 2}
@@ -90,6 +90,8 @@ def load_library(path: str = LIB_PATH):
         L.ik_fk.argtypes = [vp, dp, i64, dp, dp, ctypes.c_int, st]
         L.ik_fabrik_solve.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp, ctypes.c_int,
                                       st]
+        L.ik_fabrik_solve_fk.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp, dp,
+                                         ctypes.c_int, st]
         L.ik_fabrik_calc.argtypes = [vp, ctypes.c_int, dp, dp, ctypes.c_int, dp, i64,
                                      ctypes.c_double, i32, dp, ip, ctypes.c_int, st]
         L.ik_ann_load.argtypes = [vp, ctypes.c_int, ip, ip, ctypes.POINTER(ctypes.c_void_p),
@@ -188,8 +190,10 @@ class Context:
 
     def fk_device(self, ang, xyz, flags: int = IK_F_DEVICE):
         s = IkStats()
-        self._check(self.lib.ik_fk(self.handle, _ptr(ang), ang.shape[0], _ptr(xyz), None,
-                                   flags, ctypes.byref(s)))
+        n = int(ang.shape[0])
+        self._check(self.lib.ik_fk(self.handle, self._dev(ang, "float64", (n, 4), "ang"), n,
+                                   self._dev(xyz, "float64", (n, 3), "xyz"), None, flags,
+                                   ctypes.byref(s)))
         return s
 
     def fabrik_solve(self, pts, tol=1e-3, max_iter=100, check_limits=True,
@@ -207,12 +211,50 @@ class Context:
                                              ctypes.byref(s)))
         return ang, it, jo, s
 
-    def fabrik_solve_device(self, pts, ang, iters=None, joints=None, tol=1e-3, max_iter=100,
-                            flags: int = IK_F_DEVICE):
+    def fabrik_solve_fk(self, pts, tol=1e-3, max_iter=100, check_limits=True):
+        """FABRIK with the FK round trip in the same launch (ik_fabrik_solve_fk):
+        returns (angles n x 4 f64, iters, fk_err n f64, stats)."""
         s = IkStats()
-        self._check(self.lib.ik_fabrik_solve(self.handle, _ptr(pts), pts.shape[0], float(tol),
-                                             int(max_iter), _ptr(ang), _ptr(iters),
-                                             _ptr(joints), flags, ctypes.byref(s)))
+        p = _host(pts, np.float64, 3)
+        n = p.shape[0]
+        ang = np.empty((n, 4), np.float64)
+        it = np.empty(n, np.int32)
+        err = np.empty(n, np.float64)
+        flags = 0 if check_limits else IK_F_NO_LIMITS
+        self._check(self.lib.ik_fabrik_solve_fk(self.handle, _ptr(p), n, float(tol),
+                                                int(max_iter), _ptr(ang), _ptr(it), None,
+                                                _ptr(err), flags, ctypes.byref(s)))
+        return ang, it, err, s
+
+    def _dev(self, t, dtype: str, shape, name: str):
+        """Checks a device tensor argument before its pointer goes to the library:
+        the kernels read raw memory of a fixed dtype and layout."""
+        if t is None:
+            return None
+        if not _is_device(t):
+            raise ValueError(f"{name}: expected a device tensor on cuda:{self.device}")
+        if str(t.dtype) != f"torch.{dtype}":
+            raise ValueError(f"{name}: dtype {t.dtype}, expected torch.{dtype}")
+        if not t.is_contiguous():
+            raise ValueError(f"{name}: must be contiguous")
+        if t.device.index != self.device:
+            raise ValueError(f"{name}: on {t.device}, the context is on cuda:{self.device}")
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+        return _ptr(t)
+
+    def fabrik_solve_device(self, pts, ang, iters=None, joints=None, tol=1e-3, max_iter=100,
+                            flags: int = IK_F_DEVICE, fk_err=None):
+        s = IkStats()
+        n = int(pts.shape[0])
+        args = (self._dev(pts, "float64", (n, 3), "pts"),
+                self._dev(ang, "float64", (n, 4), "ang"),
+                self._dev(iters, "int32", (n,), "iters"),
+                self._dev(joints, "float64", (n, 4, 3), "joints"),
+                self._dev(fk_err, "float64", (n,), "fk_err"))
+        self._check(self.lib.ik_fabrik_solve_fk(self.handle, args[0], n, float(tol),
+                                                int(max_iter), args[1], args[2], args[3],
+                                                args[4], flags, ctypes.byref(s)))
         return s
 
     def fabrik_calc(self, dists, init, goals, tol=1e-3, max_iter=100):
@@ -275,8 +317,11 @@ class Context:
 
     def ann_solve_device(self, pts, ang, fk_err=None, flags: int = IK_F_DEVICE):
         s = IkStats()
-        self._check(self.lib.ik_ann_solve(self.handle, _ptr(pts), pts.shape[0], _ptr(ang),
-                                          _ptr(fk_err), flags, ctypes.byref(s)))
+        n = int(pts.shape[0])
+        self._check(self.lib.ik_ann_solve(self.handle, self._dev(pts, "float64", (n, 3), "pts"), n,
+                                          self._dev(ang, "float32", (n, 4), "ang"),
+                                          self._dev(fk_err, "float64", (n,), "fk_err"), flags,
+                                          ctypes.byref(s)))
         return s
 
     def set_timing(self, on: bool = True):

@@ -700,35 +700,6 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
   }
 }
 
-// The FK round trip of one point (cli.py:54-61 + the distance to the target),
-// register-lean: the effector is Rz(t1) B1 Rz(t2) B2 Rz(t3) B3 Rz(t4) B4 e4
-// with B_i = Tz(d_i) Tx(a_i) Rx(alpha_i) (forward.py:63-70 regrouped),
-// applied right to left to a vector; jc[i] = {a_i, d_i, cos alpha_i, sin alpha_i}
-// from the host.  Same value as fk_chain up to rounding (~1e-15).
-__device__ __forceinline__ double fk_error(const double *jc, const double th[4], double px,
-                                           double py, double pz, int alpha_bad) {
-  bool ok = !alpha_bad;
-  double x = jc[12], y = 0.0, z = jc[13];  // B4 e4 = (a4, 0, d4)
-#pragma unroll
-  for (int i = 3; i >= 0; --i) {
-    ok = ok && angle_ok(th[i]);
-    double s, c;
-    sincos(th[i], &s, &c);
-    double xr = c * x - s * y, yr = s * x + c * y;  // Rz(t_i)
-    x = xr;
-    y = yr;
-    if (i > 0) {  // B_{i} (1-based), i.e. jc[i - 1]
-      const double *b = jc + 4 * (i - 1);
-      double yb = b[2] * y - b[3] * z, zb = b[3] * y + b[2] * z + b[1];
-      x = x + b[0];
-      y = yb;
-      z = zb;
-    }
-  }
-  d3 e = {x, y, z}, p = {px, py, pz};
-  return ok ? dist3(e, p) : __builtin_nan("");
-}
-
 // X: 0 fp32; 1 bf16x6, 2 fp16x3 -- layers whose split weight operand exists
 // (a.m.wx[l]) take the split GEMM; the others (input layer, split-K output
 // layer, fp16x3-ineligible layers) stay fp32.
@@ -836,16 +807,10 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
     __syncthreads();  // the next tile's staging overwrites H
     stamp(stp ? stp + kStampSlots - 1 : nullptr);
   }
-  // per-block FK-error stats: one atomic pair per wave holding points, into its shard
-  if (a.fk_err && tid < BM) {
-    double mx = wave_max_f64(blk_max);
-    double sm = wave_sum_f64(blk_sum);
-    if (lane == 0) {
-      const int sh = blockIdx.x % kStatShards;
-      atomicMax(&a.S->max_fk_err_bits[sh], (unsigned long long)__double_as_longlong(mx));
-      atomicAdd(&a.S->sum_fk_err[sh], sm);
-    }
-  }
+  // per-block FK-error stats: one atomic pair per wave holding points, into its shard.
+  // The whole wave reduces (lanes >= BM hold zeros): at MR = 1 the upper half of
+  // wave 0 holds no points but its registers take part in the shuffles.
+  if (a.fk_err && wave * 64 < BM) wave_fk_stats(a.S, blk_max, blk_sum);
 }
 
 // The bf16x6 kernels are instantiated in a translation unit of their own
@@ -999,15 +964,7 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   a.check_limits = check_limits ? 1 : 0;
   a.S = S;
   a.dbg = dbg;
-  a.alpha_bad = 0;
-  for (int i = 0; i < 4; ++i) {
-    const double al = r.dh[12 + i];
-    a.jc[4 * i + 0] = r.dh[8 + i];  // a_i
-    a.jc[4 * i + 1] = r.dh[4 + i];  // d_i
-    a.jc[4 * i + 2] = std::cos(al);
-    a.jc[4 * i + 3] = std::sin(al);
-    if (al < -2 * kPi || al > 2 * kPi) a.alpha_bad = 1;
-  }
+  fk_trip_consts(r, a.jc, &a.alpha_bad);
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||

@@ -394,6 +394,12 @@ int ik_fk(ik_ctx *c, const double *ang, int64_t n, double *xyz, double *mats, in
 
 int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t max_iter,
                     double *ang, int32_t *iters, double *joints, int flags, ik_stats *stats) {
+  return ik_fabrik_solve_fk(c, pts, n, tol, max_iter, ang, iters, joints, nullptr, flags, stats);
+}
+
+int ik_fabrik_solve_fk(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t max_iter,
+                       double *ang, int32_t *iters, double *joints, double *fk_err, int flags,
+                       ik_stats *stats) {
   if (!c || n < 0 || (n > 0 && (!pts || !ang)) || max_iter < 0)
     return fail(IK_E_BADARG, "ik_fabrik_solve: bad args");
   if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
@@ -409,11 +415,12 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
   size_t b_ang = dev ? 0 : Stage::up((size_t)n * 32);
   size_t b_it = (dev || !iters) ? 0 : Stage::up((size_t)n * 4);
   size_t b_jo = (dev || !joints) ? 0 : Stage::up((size_t)n * 96);
-  if ((rc = ensure_scratch(c, b_work + b_in + b_ang + b_it + b_jo))) return rc;
+  size_t b_fe = (dev || !fk_err) ? 0 : Stage::up((size_t)n * 8);
+  if ((rc = ensure_scratch(c, b_work + b_in + b_ang + b_it + b_jo + b_fe))) return rc;
   char *s = static_cast<char *>(c->scratch);
   void *work = s;
   const double *dp = pts;
-  double *da = ang, *dj = joints;
+  double *da = ang, *dj = joints, *dfe = fk_err;
   int32_t *di = iters;
   if (!dev) {
     char *q = s + b_work;
@@ -425,9 +432,11 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
     di = iters ? reinterpret_cast<int32_t *>(q) : nullptr;
     q += b_it;
     dj = joints ? reinterpret_cast<double *>(q) : nullptr;
+    q += b_jo;
+    dfe = fk_err ? reinterpret_cast<double *>(q) : nullptr;
   }
   launch_reset_stats(c->d_stats, c->stream);
-  launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj,
+  launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj, dfe,
                       !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
                       c->fabrik_variant, c->fabrik_core, c->fab_ord, c->rconst,
                       c->dbg, c->fabrik_bpc);
@@ -438,6 +447,8 @@ int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t
       IK_HIP(hipMemcpyAsync(iters, di, (size_t)n * 4, hipMemcpyDeviceToHost, c->stream));
     if (joints)
       IK_HIP(hipMemcpyAsync(joints, dj, (size_t)n * 96, hipMemcpyDeviceToHost, c->stream));
+    if (fk_err)
+      IK_HIP(hipMemcpyAsync(fk_err, dfe, (size_t)n * 8, hipMemcpyDeviceToHost, c->stream));
   }
   return finish(c, flags, stats);
 }

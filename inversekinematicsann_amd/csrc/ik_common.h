@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cmath>
+
 #include "../../include/ikhip.h"
 
 namespace ikhip {
@@ -23,11 +25,17 @@ constexpr double kPi = 3.141592653589793;  // math.pi
 // shard blockIdx % kStatShards, so no single word takes more than a few
 // hundred atomics per launch; the host folds the shards.
 constexpr int kStatShards = 64;
+constexpr int kOrdClasses = 16;  // FABRIK work-order cost classes (queue order: hardest first)
+constexpr int kOrdShards = 16;   // ... and the counter shards per class (blocks b % kOrdShards)
 struct DevStats {
   unsigned long long first_oob;      // atomicMin of point index
   unsigned long long first_err_key;  // atomicMin of (index << 8) | code
   unsigned long long queue;          // work-queue head (persistent kernels)
-  unsigned long long pad0;
+  unsigned long long ticket;         // blocks of the FABRIK iteration kernel that finished
+  // FABRIK work order: points per (cost class, block shard), and the scatter's
+  // cursor inside each (class, shard) region of the queue
+  unsigned int cls_tot[kOrdClasses][kOrdShards];
+  unsigned int cls_cur[kOrdClasses][kOrdShards];
   unsigned long long sum_iters[kStatShards];
   unsigned long long n_capped[kStatShards];
   unsigned long long max_fk_err_bits[kStatShards];  // atomicMax on non-negative double bits
@@ -253,8 +261,15 @@ __device__ __forceinline__ int fk_chain(const double *dh, const double th[4], d3
 struct RobotConstDev {
   double A[3][16];  // dh_transform(dh[k], dh[4+k], dh[8+k], dh[12+k]), k = 1..3
   double ca1, sa1;  // cos / sin(alpha_1)
+  double d1, a1;    // dh[4], dh[8]: Tz / Tx of A_1
+  double lim[6];    // workspace limits (inverse.py:26-35)
+  double jc[16];    // fk_error's per-joint constants (fk_trip_consts)
+  int alpha_bad;
   int st;           // fk_chain's angle check of the constant angles
 };
+// The robot constants through the constant address space: wave-uniform
+// s_load_dwordx* into SGPRs instead of vector loads per lane.
+typedef const RobotConstDev __attribute__((address_space(4))) *RcConst;
 
 // Rows 0-2 of C = A * B, each element the same k-ordered FMA chain as mm4.
 // Rows 0-2 of a product only read rows 0-2 of its left factor, and the chain
@@ -276,21 +291,19 @@ __device__ __forceinline__ void mm4_r3(const double *A, const double *B, double 
 
 // fk_chain(dh, {th1, dh[1], dh[2], dh[3]}, J), bit for bit, from the constants:
 // A_1 = ((Rz(th1) Tz(d_1)) Tx(a_1)) Rx(alpha_1) and M_k = M_{k-1} A_k, rows 0-2.
-__device__ __forceinline__ int seed_chain(const double *dh, const RobotConstDev *rc,
-                                          double th1, d3 J[4]) {
+__device__ __forceinline__ int seed_chain(const RobotConstDev *rc, double th1, d3 J[4]) {
+  // the constants are read through the constant address space: wave-uniform
+  // s_load_dwordx* into SGPRs instead of 25 vector loads per lane, each a
+  // memory round trip on the seed's critical path
+  const RcConst k = (RcConst)rc;
   double R[16], T1[16], T2[16], X[16], M[12];
   const double c = cos(th1), s = sin(th1);
   ident4(R);
   R[0] = c; R[1] = -s; R[4] = s; R[5] = c;
   ident4(T1);
-  T1[11] = dh[4];
+  T1[11] = k->d1;
   ident4(T2);
-  T2[3] = dh[8];
-  // the constants are read through the constant address space: wave-uniform
-  // s_load_dwordx* into SGPRs instead of 25 vector loads per lane, each a
-  // memory round trip on the seed's critical path (seed kernel VALU 28 % busy)
-  typedef const RobotConstDev __attribute__((address_space(4))) *RcConst;
-  const RcConst k = (RcConst)rc;
+  T2[3] = k->a1;
   ident4(X);
   const double ca1 = k->ca1, sa1 = k->sa1;
   X[5] = ca1; X[6] = -sa1; X[9] = sa1; X[10] = ca1;
@@ -307,6 +320,35 @@ __device__ __forceinline__ int seed_chain(const double *dh, const RobotConstDev 
     J[i].x = M[3]; J[i].y = M[7]; J[i].z = M[11];
   }
   return k->st;
+}
+
+// The FK round trip of one point (cli.py:54-61 + the distance to the target),
+// register-lean: the effector is Rz(t1) B1 Rz(t2) B2 Rz(t3) B3 Rz(t4) B4 e4
+// with B_i = Tz(d_i) Tx(a_i) Rx(alpha_i) (forward.py:63-70 regrouped),
+// applied right to left to a vector; jc[i] = {a_i, d_i, cos alpha_i, sin alpha_i}
+// from the host (fk_trip_consts).  Same value as fk_chain up to rounding (~1e-15).
+__device__ __forceinline__ double fk_error(const double *jc, const double th[4], double px,
+                                           double py, double pz, int alpha_bad) {
+  bool ok = !alpha_bad;
+  double x = jc[12], y = 0.0, z = jc[13];  // B4 e4 = (a4, 0, d4)
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    ok = ok && angle_ok(th[i]);
+    double s, c;
+    sincos_fk(th[i], &s, &c);  // |th| <= 2 pi here (ok); outside, the result is NaN anyway
+    double xr = c * x - s * y, yr = s * x + c * y;  // Rz(t_i)
+    x = xr;
+    y = yr;
+    if (i > 0) {  // B_{i} (1-based), i.e. jc[i - 1]
+      const double *b = jc + 4 * (i - 1);
+      double yb = b[2] * y - b[3] * z, zb = b[3] * y + b[2] * z + b[1];
+      x = x + b[0];
+      y = yb;
+      z = zb;
+    }
+  }
+  d3 e = {x, y, z}, p = {px, py, pz};
+  return ok ? dist3(e, p) : __builtin_nan("");
 }
 
 // Same chain, writing all four cumulative transforms (row-major 4x4 each).
@@ -363,12 +405,11 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 
 // Block-wide FABRIK iteration stats (blockDim 256): one atomic per counter per
 // block, into the block's shard.  Every thread of the block must call it.
-__device__ __forceinline__ void block_iter_stats(DevStats *S, bool valid, int it, int max_iter) {
+// s / c / m: this thread's iteration sum, capped-point count and largest count.
+__device__ __forceinline__ void block_iter_stats_acc(DevStats *S, unsigned long long s,
+                                                     unsigned long long c, int m) {
   __shared__ unsigned long long red_s[4], red_c[4];
   __shared__ int red_m[4];
-  unsigned long long s = valid ? (unsigned long long)it : 0ull;
-  unsigned long long c = (valid && it >= max_iter) ? 1ull : 0ull;
-  int m = valid ? it : 0;
   s = wave_sum_u64(s);
   c = wave_sum_u64(c);
   m = wave_max_i32(m);
@@ -393,6 +434,23 @@ __device__ __forceinline__ void block_iter_stats(DevStats *S, bool valid, int it
   }
 }
 
+__device__ __forceinline__ void block_iter_stats(DevStats *S, bool valid, int it, int max_iter) {
+  block_iter_stats_acc(S, valid ? (unsigned long long)it : 0ull,
+                       (valid && it >= max_iter) ? 1ull : 0ull, valid ? it : 0);
+}
+
+// FK round-trip error stats: one atomic pair per wave into the block's shard.
+// mx / sm: this lane's largest and summed finite errors.  The whole wave calls it.
+__device__ __forceinline__ void wave_fk_stats(DevStats *S, double mx, double sm) {
+  mx = wave_max_f64(mx);
+  sm = wave_sum_f64(sm);
+  if ((threadIdx.x & 63) == 0) {
+    const int sh = blockIdx.x % kStatShards;
+    atomicMax(&S->max_fk_err_bits[sh], (unsigned long long)__double_as_longlong(mx));
+    atomicAdd(&S->sum_fk_err[sh], sm);
+  }
+}
+
 }  // namespace ikhip
 
 // Launchers implemented in the .hip files and called by ik_api.cpp.
@@ -402,6 +460,20 @@ struct RobotDev {
   double links[4];
   double lim[6];
 };
+
+// Host: the per-joint constants of fk_error, {a_i, d_i, cos alpha_i, sin alpha_i},
+// and whether some |alpha_i| > 2 pi (then FK raises for every point, forward.py:23-25).
+inline void fk_trip_consts(const RobotDev &r, double jc[16], int *alpha_bad) {
+  *alpha_bad = 0;
+  for (int i = 0; i < 4; ++i) {
+    const double al = r.dh[12 + i];
+    jc[4 * i + 0] = r.dh[8 + i];
+    jc[4 * i + 1] = r.dh[4 + i];
+    jc[4 * i + 2] = std::cos(al);
+    jc[4 * i + 3] = std::sin(al);
+    if (al < -2 * kPi || al > 2 * kPi) *alpha_bad = 1;
+  }
+}
 
 // Optional per-kernel HIP-event timing of the current call (ik_ctx_set_timing):
 // launchers bracket every kernel with kt_begin / kt_end.
@@ -419,27 +491,25 @@ void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, dou
 constexpr int kOrdCellsR = 64, kOrdCellsE = 16, kOrdCells = kOrdCellsR * kOrdCellsE;
 constexpr int kOrdSample = 256;           // 1 point in 256 is recorded ...
 constexpr int kOrdMaxSample = 1 << 14;    // ... up to this many per call
-constexpr int kOrdClasses = 16;           // cost classes (queue order: hardest first)
-constexpr int kOrdMaxSeg = 2048;          // point segments of the class histogram
 struct FabOrderDev {
   unsigned int key[kOrdCells];  // 1 + largest recorded iterations per cell, 0 = unseen
-  unsigned int nsample;         // (cell << 16 | iterations) records of the call
-  unsigned int sample[kOrdMaxSample];
-  unsigned int hist[kOrdClasses * kOrdMaxSeg];  // class counts, then scatter cursors
+  unsigned int sample[kOrdMaxSample];  // (cell << 16 | iterations) records of the call
 };
 
 // FABRIK ikine.  scratch must hold fabrik_scratch_bytes(n).  ord: the
 // context's cost table (zero-initialised once), or null for queue order =
-// point order.
+// point order.  fk_err (nullable): |FK(theta) - p| per point, max/sum into S.
 size_t fabrik_scratch_bytes(int64_t n);
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
-                         bool check_limits, void *scratch, DevStats *S, hipStream_t st,
+                         double *fk_err, bool check_limits, void *scratch, DevStats *S, hipStream_t st,
                          int variant, int core, FabOrderDev *ord, const RobotConstDev *rc,
                          unsigned long long *dbg, int bpc = 0);
 constexpr size_t kFabrikDebugWords = 64 + 4 * 4000;  // diagnostic build counters
 // Per-robot seed constants (RobotConstDev) into device memory, on stream st.
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t st);
+// The robot constants of the last launch_robot_const, for an unchanged robot.
+bool robot_const_current(const RobotDev &r);
 void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,
                         const double *goals, int64_t n, double tol, int max_iter,
                         double *joints, int32_t *iters, DevStats *S, hipStream_t st);

@@ -7,10 +7,12 @@
 // with the same operation order, so iteration counts are bit-exact.
 //
 // Two pipelines (DESIGN.md "FABRIK"):
-//  * split (default): seed_kernel (limits + FK seed pose) -> iter_kernel
-//    (persistent; a lane whose point converged is refilled from a per-wave
-//    chunk of a global work queue, so a wave no longer waits for its slowest
-//    lane) -> angles_kernel (law of cosines + per-batch stats).
+//  * fused (default): classify + scatter (the hard-first work order, 6 bytes
+//    per point) -> iter_kernel: persistent; each wave prepares batches of seed
+//    poses in registers, refills a lane whose point converged from them (so a
+//    wave no longer waits for its slowest lane), parks finished lanes in LDS and
+//    runs the angles step + FK round trip + batch stats on them in batches.
+//    Seed poses and final joints never touch HBM.
 //  * simple: everything in one kernel, one point per lane, no refill.
 // Per point the state is 4 joints + goal (15 doubles) held in VGPRs.
 #include <atomic>
@@ -160,12 +162,18 @@ __device__ __forceinline__ void get_angles(const d3 J[4], double th[4], int &st)
 // Seed pose, inverse.py:123-130: FK of [atan2(y, x), thetas[1:]] (the
 // reference writes theta_1 into dh_matrix[0][0] and runs fkine on that row),
 // through the per-robot constants (seed_chain; same bits as fk_chain).
-__device__ __forceinline__ int seed_pose(const RobotDev &r, const RobotConstDev *rc, d3 g,
-                                         d3 J[4]) {
-  return seed_chain(r.dh, rc, atan2(g.y, g.x), J);
+__device__ __forceinline__ int seed_pose(const RobotConstDev *rc, d3 g, d3 J[4]) {
+  return seed_chain(rc, atan2(g.y, g.x), J);
 }
 
-__global__ void robot_const_kernel(RobotDev r, RobotConstDev *rc) {
+// The per-robot constants (RobotConstDev).  jc / alpha_bad come from the host
+// (fk_trip_consts: the values the ANN kernel's round trip uses too).
+struct FkTrip {
+  double jc[16];
+  int alpha_bad;
+};
+
+__global__ void robot_const_kernel(RobotDev r, FkTrip t, RobotConstDev *rc) {
   if (threadIdx.x != 0) return;
   int st = IK_OK;
   for (int k = 1; k < 4; ++k) {
@@ -177,11 +185,18 @@ __global__ void robot_const_kernel(RobotDev r, RobotConstDev *rc) {
   const double al = r.dh[12];
   rc->ca1 = cos(al);
   rc->sa1 = sin(al);
+  rc->d1 = r.dh[4];
+  rc->a1 = r.dh[8];
+  for (int k = 0; k < 6; ++k) rc->lim[k] = r.lim[k];
+  for (int k = 0; k < 16; ++k) rc->jc[k] = t.jc[k];
+  rc->alpha_bad = t.alpha_bad;
   rc->st = st;
 }
 
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t stream) {
-  hipLaunchKernelGGL(robot_const_kernel, dim3(1), dim3(64), 0, stream, r, rc);
+  FkTrip t;
+  fk_trip_consts(r, t.jc, &t.alpha_bad);
+  hipLaunchKernelGGL(robot_const_kernel, dim3(1), dim3(64), 0, stream, r, t, rc);
 }
 
 __device__ __forceinline__ void store_joints(double *dst, int64_t i, const d3 J[4]) {
@@ -214,18 +229,15 @@ struct FabArgs {
   int max_iter;
   int check_limits;
   double *ang;
-  int32_t *iters;
-  double *joints;  // final joints (n x 12); never null in the split pipeline
-  double *seeds;   // split pipeline scratch (n x 12)
-  uint8_t *status; // split pipeline scratch (n)
+  int32_t *iters;   // nullable
+  double *joints;   // final joints n x 12 (nullable)
+  double *fk_err;   // |FK(theta) - p| per point (nullable; max/sum into S)
   DevStats *S;
-  int chunk;       // work-queue grab size of the persistent iteration kernel
+  int chunk;        // work-queue grab size of the persistent iteration kernel (1..64)
   // hard-first ordering (see "Work order" below); unused when perm is null
-  int32_t *perm;            // queue position -> point index
-  uint8_t *status_in;       // ordered: the seed status by point
-  uint16_t *cell;           // per point: goal cell (bits 0-9) | cost class << 10
-  FabOrderDev *ord;         // context-owned cost table and class histogram
-  int nseg, seg_blocks;     // histogram segments, and blocks per segment
+  int32_t *perm;    // queue position -> point index
+  uint16_t *cell;   // per point: goal cell (bits 0-9) | cost class << 10
+  FabOrderDev *ord; // context-owned cost table
   unsigned long long *dbg;  // diagnostic build only: iteration-kernel counters
 };
 
@@ -234,7 +246,7 @@ struct FabArgs {
 // dbg[64 + 4w ..]: s_memrealtime (100 MHz) at start, when the queue ran dry
 // for it and at the end, and the steps it ran after the queue ran dry.
 enum { kDiagLoops, kDiagSteps, kDiagLaneSteps, kDiagRefills, kDiagGrabs, kDiagFallbacks,
-       kDiagWaves, kDiagCount };
+       kDiagWaves, kDiagFlushes, kDiagFlushTicks, kDiagPrepTicks, kDiagCount };
 #ifdef IKHIP_DIAG
 constexpr int kDiagWaveMax = 4000;  // = (kFabrikDebugWords - 64) / 4
 #endif
@@ -244,18 +256,78 @@ static int env_int(const char *name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
+// The angles step of one finished point (inverse.py:136 __get_angles) and what
+// the call reports about it: angles, iterations, joints, the FK round trip
+// (cli.py:54-61) and the per-lane sums of the batch stats.
+struct LaneAcc {
+  unsigned long long sum_it = 0, capped = 0;
+  int max_it = 0;
+  double fk_max = 0.0, fk_sum = 0.0;
+};
+
+// The robot constants' pointer made opaque to the compiler: loads through it are
+// issued where they are used (s_load, scalar cache) instead of hoisted out of the
+// persistent loop into SGPRs, where the seed and angles steps' ~100 constants
+// spilled and the iteration paid for their reloads (v_readlane) every step.
+__device__ __forceinline__ RcConst opaque_rc(const RobotConstDev *p) {
+  asm volatile("" : "+s"(p));
+  return (RcConst)p;
+}
+
+__device__ __forceinline__ bool outside_rc(RcConst k, d3 g) {
+  const double lim[6] = {k->lim[0], k->lim[1], k->lim[2], k->lim[3], k->lim[4], k->lim[5]};
+  return outside(lim, g.x, g.y, g.z);
+}
+
+__device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const d3 J[4], int it,
+                                             int st, LaneAcc &acc) {
+  double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
+#ifndef IKHIP_EXP_NOANGLES
+  if (st == IK_OK) get_angles(J, th, st);
+#else
+  th[0] = J[3].x; th[1] = J[3].y; th[2] = J[3].z; th[3] = J[2].x;
+#endif
+  if (st != IK_OK) record_error(a.S, i, st);
+  double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
+  o[0] = make_double2(th[0], th[1]);
+  o[1] = make_double2(th[2], th[3]);
+  if (a.iters) a.iters[i] = it;
+  if (a.joints) store_joints(a.joints, i, J);
+  acc.sum_it += (unsigned long long)it;
+  acc.capped += (it >= a.max_iter) ? 1ull : 0ull;
+  acc.max_it = max(acc.max_it, it);
+  if (a.fk_err) {
+    double e = __builtin_nan("");
+    if (st == IK_OK) {
+      const RcConst k = opaque_rc(a.rc);
+      double jc[16];
+#pragma unroll
+      for (int e2 = 0; e2 < 16; ++e2) jc[e2] = k->jc[e2];
+      e = fk_error(jc, th, a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2], k->alpha_bad);
+    }
+    a.fk_err[i] = e;
+    if (e == e) {
+      acc.fk_max = fmax(acc.fk_max, e);
+      acc.fk_sum += e;
+    }
+  }
+}
+
 // ------------------------------------------------------------- simple ----
+// One point per lane, no refill: the test variant (IKHIP_FABRIK_VARIANT=0) and
+// the solves whose loop runs no iteration at all (max_iter 0, tol >= 1) or whose
+// robot FK rejects (its own DH angles out of range: every seed raises).
 __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool valid = i < a.n;
-  int it = 0;
-  if (valid) {
+  LaneAcc acc;
+  if (i < a.n) {
     d3 g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
     if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
       atomicMin(&a.S->first_oob, (unsigned long long)i);
     d3 J[4];
-    int st = seed_pose(a.r, a.rc, g, J);
+    int st = seed_pose(a.rc, g, J);
     double se = 1.0, ge = 1.0;
+    int it = 0;
     if (st == IK_OK) {
       while (((se > a.tol2) || (ge > a.tol2)) && (a.max_iter > it)) {
         fabrik_step4(J[0], J[1], J[2], J[3], g, a.r.links, se, ge, st);
@@ -263,23 +335,11 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
         if (st != IK_OK) break;
       }
     }
-    double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
-    if (st == IK_OK) get_angles(J, th, st);
-    if (st != IK_OK) record_error(a.S, i, st);
-    double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
-    o[0] = make_double2(th[0], th[1]);
-    o[1] = make_double2(th[2], th[3]);
-    if (a.iters) a.iters[i] = it;
-    if (a.joints) store_joints(a.joints, i, J);
+    finish_point(a, i, J, it, st, acc);
   }
-  block_iter_stats(a.S, valid, it, a.max_iter);
+  block_iter_stats_acc(a.S, acc.sum_it, acc.capped, acc.max_it);
+  if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
 }
-
-// -------------------------------------------------------------- split ----
-// 1. limits + seed pose (uniform work, one point per lane).  ORD (work order
-// below): also the goal's cell and the per-segment counts of its cost class.
-template <bool ORD>
-__global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a);
 
 // ---------------------------------------------------------- Work order ----
 // The persistent iteration kernel hands points out in queue order.  In point
@@ -287,8 +347,8 @@ __global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a);
 // and set the launch length alone (≈ 1.4x the lane-iterations / lanes bound
 // at 1M random_dist points).  Handing out the expensive points first removes
 // most of that tail.  The cost of a point is predicted from its goal cell --
-// distance from the shoulder (the first joint) in 64 bins up to the reach of
-// links 1..3, and the sine of the elevation in 16 bins -- by the LARGEST
+// distance from the shoulder (the seed's first joint) in 64 bins up to the reach
+// of links 1..3, and the sine of the elevation in 16 bins -- by the LARGEST
 // iteration count the context recorded in that cell on earlier calls (1 point
 // in kOrdSample; the old key decays by 1/8 when new records arrive).  The
 // largest, not the mean: what sets the tail is a long point starting late, and
@@ -302,16 +362,19 @@ __global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a);
 // permutation.  Results do not depend on the order: every point is still
 // solved by the same arithmetic on its own.
 //
-// Launches: seed (+ class counts) -> scan (1 block; + folds the previous
-// call's records into the table) -> scatter -> iterate -> angles (+ records,
-// + clears the class counts).  (Doing the one-block steps in the last block of
-// the kernel before, found with a ticket counter, measured 0.6 ms: 4k
-// same-address returning atomics.)
-constexpr int kOrdSegBlocksMin = 16;  // histogram segment: >= 16 blocks of 256 points
+// Launches: classify (cell + class per point from the goal alone, class totals)
+// -> scatter (class region starts from the totals, one cursor per class: the
+// queue -> point permutation) -> iterate (the last block to finish folds this
+// call's records into the table for the next call).
+constexpr int kOrdPPT = 8;  // points per thread of the classify / scatter blocks
 
-__device__ __forceinline__ int goal_cell(const RobotDev &r, d3 g, d3 shoulder) {
-  const double dx = g.x - shoulder.x, dy = g.y - shoulder.y, dz = g.z - shoulder.z;
-  const double dist = sqrt(dx * dx + dy * dy + dz * dz);
+// The shoulder (the seed's first joint, the translation of A_1) is
+// (a1 cos t1, a1 sin t1, d1) with t1 the goal's own azimuth: its distance from the
+// goal needs no trigonometry.
+__device__ __forceinline__ int goal_cell(const RobotDev &r, d3 g) {
+  const double rxy = sqrt(g.x * g.x + g.y * g.y) - r.dh[8];
+  const double dz = g.z - r.dh[4];
+  const double dist = sqrt(rxy * rxy + dz * dz);
   const double reach = r.links[1] + r.links[2] + r.links[3];
   int rb = (int)(dist / reach * kOrdCellsR);
   rb = rb < 0 ? 0 : (rb >= kOrdCellsR ? kOrdCellsR - 1 : rb);
@@ -327,62 +390,19 @@ __device__ __forceinline__ int cost_class(const FabOrderDev *T, int cell, int ma
   return k < 0 ? 0 : (k >= kOrdClasses ? kOrdClasses - 1 : k);
 }
 
-// Exclusive scan of the class counts in queue order (hardest class first,
-// then segment), in place: hist becomes the per-(class, segment) cursors the
-// scatter advances.  One block.
-__device__ void order_scan(FabOrderDev *T, int nseg) {
-  __shared__ uint32_t part[256];
-  const int t = threadIdx.x;
-  const int E = kOrdClasses * nseg;
-  const int per = (E + 255) / 256, b0 = t * per, b1 = min(E, b0 + per);
-  // scan position e = class (kOrdClasses-1 - e / nseg), segment e % nseg
-  auto at = [&](int e) { return (kOrdClasses - 1 - e / nseg) * nseg + e % nseg; };
-  // the counts are read kScanBatch at a time with independent loads (a plain
-  // loop waits out one memory latency per entry: 15 us per call at 1M points)
-  constexpr int kScanBatch = 16;
-  uint32_t s = 0;
-  for (int e0 = b0; e0 < b1; e0 += kScanBatch) {
-    uint32_t v[kScanBatch];
-#pragma unroll
-    for (int j = 0; j < kScanBatch; ++j) v[j] = (e0 + j < b1) ? T->hist[at(e0 + j)] : 0u;
-#pragma unroll
-    for (int j = 0; j < kScanBatch; ++j) s += v[j];
-  }
-  part[t] = s;
-  __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {  // inclusive Hillis-Steele scan
-    const uint32_t v = (t >= d) ? part[t - d] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  uint32_t run = part[t] - s;
-  for (int e0 = b0; e0 < b1; e0 += kScanBatch) {
-    uint32_t v[kScanBatch];
-#pragma unroll
-    for (int j = 0; j < kScanBatch; ++j) v[j] = (e0 + j < b1) ? T->hist[at(e0 + j)] : 0u;
-#pragma unroll
-    for (int j = 0; j < kScanBatch; ++j) {
-      if (e0 + j < b1) T->hist[at(e0 + j)] = run;
-      run += v[j];
-    }
-  }
-}
-
-// Fold the records into the table: per cell, the largest recorded iteration
+// Fold ns records into the table: per cell, the largest recorded iteration
 // count of the call, or the decayed old key if larger.  One block.
-__device__ void order_fold(FabOrderDev *T) {
+__device__ void order_fold(FabOrderDev *T, unsigned int ns) {
   __shared__ unsigned int lm[kOrdCells];
   const int t = threadIdx.x;
-  for (int c = t; c < kOrdCells; c += 256) lm[c] = 0;
+  for (int c = t; c < kOrdCells; c += blockDim.x) lm[c] = 0;
   __syncthreads();
-  const unsigned int ns = T->nsample < kOrdMaxSample ? T->nsample : kOrdMaxSample;
-  constexpr int kFoldBatch = 8;  // independent loads in flight (as in order_scan)
-  for (unsigned int k0 = t; k0 < ns; k0 += 256 * kFoldBatch) {
+  constexpr int kFoldBatch = 8;  // independent loads in flight
+  for (unsigned int k0 = t; k0 < ns; k0 += blockDim.x * kFoldBatch) {
     unsigned int v[kFoldBatch];
 #pragma unroll
     for (int j = 0; j < kFoldBatch; ++j) {
-      const unsigned int k = k0 + 256u * j;
+      const unsigned int k = k0 + blockDim.x * j;
       v[j] = k < ns ? T->sample[k] : 0xffffffffu;
     }
 #pragma unroll
@@ -390,108 +410,177 @@ __device__ void order_fold(FabOrderDev *T) {
       if (v[j] != 0xffffffffu) atomicMax(&lm[v[j] >> 16], (v[j] & 0xffffu) + 1u);
   }
   __syncthreads();
-  for (int c = t; c < kOrdCells; c += 256) {
+  for (int c = t; c < kOrdCells; c += blockDim.x) {
     if (lm[c]) {
       const unsigned int old = T->key[c];
       const unsigned int dec = old - (old >> 3);
       T->key[c] = lm[c] > dec ? lm[c] : dec;
     }
   }
-  if (t == 0) T->nsample = 0;
 }
 
-// One block: this call's class counts -> cursors, then the previous call's
-// records -> the table (which the next call's seed kernel reads: the table
-// lags one call, which costs nothing but saves a launch).
-__global__ __launch_bounds__(256) void fabrik_order_scan_kernel(FabOrderDev *T, int nseg) {
-  order_scan(T, nseg);
-  __syncthreads();
-  order_fold(T);
-}
-
-template <bool ORD>
-__global__ __launch_bounds__(256) void fabrik_seed_kernel(FabArgs a) {
+// 1. classify: the goal's cell and cost class per point (2 bytes), and the
+// class totals (one atomic per class and block, into the block's shard: one
+// address per class took ~1k same-address atomics per launch at 1M points).
+// The cell -> class map of this call is built in LDS first.
+__global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
   __shared__ unsigned int cnt[kOrdClasses];
+  __shared__ uint8_t cls[kOrdCells];
   const int t = threadIdx.x;
-  if (ORD) {
-    if (t < kOrdClasses) cnt[t] = 0;
-    __syncthreads();
+  if (t < kOrdClasses) cnt[t] = 0;
+  for (int c = t; c < kOrdCells; c += 256) cls[c] = (uint8_t)cost_class(a.ord, c, a.max_iter);
+  const int64_t b0 = (int64_t)blockIdx.x * (256 * kOrdPPT);
+  d3 g[kOrdPPT];
+#pragma unroll
+  for (int j = 0; j < kOrdPPT; ++j) {  // all loads in flight before the first use
+    const int64_t i = b0 + j * 256 + t;
+    if (i < a.n) g[j] = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
   }
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
-  if (i < a.n) {
-    d3 g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
-    if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
-      atomicMin(&a.S->first_oob, (unsigned long long)i);
-    d3 J[4];
-    int st = seed_pose(a.r, a.rc, g, J);
-    store_joints(a.seeds, i, J);
-    if constexpr (ORD) {
-      a.status_in[i] = (uint8_t)st;
-      const int cell = goal_cell(a.r, g, J[0]);
-      const int k = cost_class(a.ord, cell, a.max_iter);
-      a.cell[i] = (uint16_t)(cell | (k << 10));  // the scatter must see this very class
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kOrdPPT; ++j) {
+    const int64_t i = b0 + j * 256 + t;
+    if (i < a.n) {
+      const int cell = goal_cell(a.r, g[j]);
+      const int k = cls[cell];
+      a.cell[i] = (uint16_t)(cell | (k << 10));
       atomicAdd(&cnt[k], 1u);
-    } else {
-      a.status[i] = (uint8_t)st;
     }
   }
-  if constexpr (ORD) {
-    __syncthreads();
-    if (t < kOrdClasses && cnt[t])
-      atomicAdd(&a.ord->hist[t * a.nseg + blockIdx.x / a.seg_blocks], cnt[t]);
-  }
+  __syncthreads();
+  if (t < kOrdClasses && cnt[t]) atomicAdd(&a.S->cls_tot[t][blockIdx.x % kOrdShards], cnt[t]);
 }
 
-// scatter: perm[cursor] = point (one point per lane; one atomic per class
-// and block claims the block's range of each class in its segment)
-__global__ __launch_bounds__(256) void fabrik_order_scatter_kernel(FabArgs a) {
-  __shared__ uint32_t wcnt[4][kOrdClasses], base[kOrdClasses];
-  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
-  const int k = (i < a.n) ? (a.cell[i] >> 10) : -1;
-  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  int rank = 0;
+// 2. scatter: perm[queue position] = point.  The queue is class-major (hardest
+// first), then shard: region (c, s) starts after every harder class and every
+// lower shard of class c.  Block b covers the points classify's block b counted
+// into shard b % kOrdShards, claims its run inside its region with one atomic
+// per class and hands the slots out through LDS atomics.
+__global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
+  __shared__ unsigned int cnt[kOrdClasses], base[kOrdClasses];
+  const int t = threadIdx.x;
+  const int sh = blockIdx.x % kOrdShards;
+  if (t < kOrdClasses) cnt[t] = 0;
+  const int64_t b0 = (int64_t)blockIdx.x * (256 * kOrdPPT);
+  uint16_t cl[kOrdPPT];
 #pragma unroll
-  for (int c = 0; c < kOrdClasses; ++c) {
-    const unsigned long long m = __ballot(k == c);
-    if (k == c) rank = __popcll(m & lt);
-    if (lane == 0) wcnt[w][c] = (uint32_t)__popcll(m);
+  for (int j = 0; j < kOrdPPT; ++j) {
+    const int64_t i = b0 + j * 256 + t;
+    cl[j] = i < a.n ? a.cell[i] : (uint16_t)0xffff;
   }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kOrdPPT; ++j)
+    if (cl[j] != 0xffff) atomicAdd(&cnt[cl[j] >> 10], 1u);
   __syncthreads();
   if (t < kOrdClasses) {
-    const uint32_t tot = wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    base[t] = tot ? atomicAdd(&a.ord->hist[t * a.nseg + blockIdx.x / a.seg_blocks], tot) : 0u;
+    unsigned int start = 0;
+    for (int c = kOrdClasses - 1; c > t; --c)
+      for (int q = 0; q < kOrdShards; ++q) start += a.S->cls_tot[c][q];
+    for (int q = 0; q < sh; ++q) start += a.S->cls_tot[t][q];
+    base[t] = start + (cnt[t] ? atomicAdd(&a.S->cls_cur[t][sh], cnt[t]) : 0u);
   }
   __syncthreads();
-  if (k >= 0) {
-    uint32_t pos = base[k] + rank;
-    for (int v = 0; v < w; ++v) pos += wcnt[v][k];
-    a.perm[pos] = (int32_t)i;
+#pragma unroll
+  for (int j = 0; j < kOrdPPT; ++j) {
+    if (cl[j] != 0xffff) {
+      const unsigned int pos = atomicAdd(&base[cl[j] >> 10], 1u);
+      a.perm[pos] = (int32_t)(b0 + j * 256 + t);
+    }
   }
 }
 
-// 2. persistent iteration with per-lane refill.
-// a.chunk: points a wave takes from the global queue at once (tuning knob,
-// IKHIP_FABRIK_CHUNK; small enough that every wave gets work at 1M points).
+// 3. persistent iteration with per-lane refill, seed and angles in batches.
+//
+// A lane whose point converged is refilled from the wave's batch of prepared
+// points: a wave grabs a.chunk queue positions at once and each lane prepares one
+// of them -- the goal, the limits check and the seed pose (inverse.py:123-130) --
+// into registers (P*), at full SIMD width; a refill then moves prepared points to
+// the free lanes with cross-lane reads (ds_bpermute), with no memory round trip.
+// A finished lane parks its final joints in the wave's LDS ring at the next
+// refill; when the ring would overflow, and at the end, the whole wave runs the
+// angles step on it, one entry per lane (finish_point).  So the seed pose and
+// the joints never travel through HBM, and neither step runs at the width of
+// the handful of lanes that finish together.
+struct RetireRing {
+  double j[12][64];
+  long long idx[64];
+  int it[64];
+  int st[64];
+};
 
-// ORD: the queue is a.perm (work order above): a refilled lane gathers its
-// point's seed pose and goal and keeps the point's index, where its results go
-// (so the angles kernel reads them in point order, coalesced).
-// CORE: 0 general sqrt / division, 1 sqrt_core / div_core, 2 the same with the
-// repeated distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
+__device__ __forceinline__ void ring_put(RetireRing &R, int s, const d3 &J0, const d3 &J1,
+                                         const d3 &J2, const d3 &J3, int64_t idx, int it,
+                                         int st) {
+  R.j[0][s] = J0.x; R.j[1][s] = J0.y; R.j[2][s] = J0.z;
+  R.j[3][s] = J1.x; R.j[4][s] = J1.y; R.j[5][s] = J1.z;
+  R.j[6][s] = J2.x; R.j[7][s] = J2.y; R.j[8][s] = J2.z;
+  R.j[9][s] = J3.x; R.j[10][s] = J3.y; R.j[11][s] = J3.z;
+  R.idx[s] = idx;
+  R.it[s] = it;
+  R.st[s] = st;
+}
+
+// The angles step over the ring's first cnt entries (the whole wave calls it).
+// ORD: 1 in kOrdSample points records (cell, iterations) for the cost table.
+template <bool ORD>
+__device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int cnt, int lane,
+                                           LaneAcc &acc) {
+  __builtin_amdgcn_wave_barrier();
+  if (lane < cnt) {
+    d3 J[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      J[k] = {R.j[3 * k][lane], R.j[3 * k + 1][lane], R.j[3 * k + 2][lane]};
+    const int64_t i = R.idx[lane];
+    const int it = R.it[lane];
+    finish_point(a, i, J, it, R.st[lane], acc);
+    if constexpr (ORD) {
+      if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
+        a.ord->sample[i / kOrdSample] = ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) |
+                                        (uint32_t)(it < 0xffff ? it : 0xffff);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ d3 shfl3(const d3 v, int src) {
+  return {__shfl(v.x, src, 64), __shfl(v.y, src, 64), __shfl(v.z, src, 64)};
+}
+
+// ORD: the queue is a.perm (work order above), else point order.  CORE: 0
+// general sqrt / division, 1 sqrt_core / div_core, 2 the same with the repeated
+// distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
+// Every solve reaching this kernel runs at least one iteration (the host sends
+// the others to fabrik_simple_kernel), so the seed's last joint is never needed.
 template <int REFILL_MIN, bool ORD, int CORE>
 __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
+  __shared__ RetireRing rings[4];
   const int lane = threadIdx.x & 63;
+  RetireRing &R = rings[threadIdx.x >> 6];
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const double tol2 = a.tol2;
   const int max_iter = a.max_iter;
   double L[4] = {a.r.links[0], a.r.links[1], a.r.links[2], a.r.links[3]};
 
-  int64_t qnext = 0, qend = 0;  // wave-uniform: indices not yet handed out
-  bool exhausted = false;
-  bool active = false;
-  int64_t idx = 0;  // queue position (= the point index unless ORD)
-  int64_t out = 0;  // the point index: where the lane's results go
+  // prepared points: lane j holds the batch's entry j (wave-uniform count / cursor)
+  d3 P0 = {0, 0, 0}, P1 = P0, P2 = P0, Pg = P0;
+  int64_t Pidx = 0;
+  int pcount = 0, pptr = 0;
+  // the next batch, fetched in stages while the current one is handed out (so
+  // that no stage waits for memory): 0 none, 1 queue grab issued (na), 2 its
+  // permutation entries loaded (nperm), 3 its goals loaded (ng, ni); -1 the queue is dry
+  int nstage = 0, ncount = 0;
+  int64_t nbase = 0;
+  unsigned long long na = 0;
+  int64_t nperm = 0, ni = 0;
+  d3 ng = {0, 0, 0};
+  bool dry = false;   // the queue and the batch are exhausted
+  int rcnt = 0;       // entries in the retire ring
+  LaneAcc acc;
+
+  bool active = false, pending = false;  // solving / finished but not yet parked
+  int64_t out = 0;                       // the lane's point index
   d3 J0 = {0, 0, 0}, J1 = J0, J2 = J0, J3 = J0, g = J0;
   double se = 1.0, ge = 1.0;
   int step = 0, st = IK_OK;
@@ -508,63 +597,121 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
 #define IKHIP_DG(k, v) ((void)0)
 #endif
   while (true) {
-    unsigned long long freem = __ballot(!active);
-    int nfree = __popcll(freem);
-    if (exhausted && nfree == 64) break;
+    const unsigned long long freem = __ballot(!active);
+    const int nfree = __popcll(freem);
+    if (dry && nfree == 64) break;
     IKHIP_DG(kDiagLoops, 1);
-    if (!exhausted && (nfree >= REFILL_MIN || nfree == 64)) {
+    if (!dry && (nfree >= REFILL_MIN || nfree == 64)) {
       IKHIP_DG(kDiagRefills, 1);
-      int rank = __popcll(freem & lt_mask);
-      int64_t mine = -1;
+      // park the lanes that finished since the last refill
+      const unsigned long long pm = __ballot(pending);
+      const int np = __popcll(pm);
+      if (np) {
+        if (rcnt + np > 64) {
+          IKHIP_DG(kDiagFlushes, 1);
+#ifdef IKHIP_DIAG
+          const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+#endif
+          ring_flush<ORD>(a, R, rcnt, lane, acc);
+#ifdef IKHIP_DIAG
+          dg[kDiagFlushTicks] += __builtin_amdgcn_s_memrealtime() - tf0;
+#endif
+          rcnt = 0;
+        }
+        if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, out, step, st);
+        pending = false;
+        rcnt += np;
+      }
+      // the next batch's stages, one per refill while the last 24 entries of this
+      // one are handed out; a stage consumes what the one before loaded (so the
+      // loads are long done), and prepare() runs the stages still missing
+      auto stage1 = [&]() {
+        if (lane == 0) na = atomicAdd(&a.S->queue, (unsigned long long)a.chunk);
+        nstage = 1;
+      };
+      auto stage2 = [&]() {
+        nbase = (int64_t)__shfl(na, 0, 64);
+        if (nbase >= a.n) {
+          nstage = -1;
+          return;
+        }
+        ncount = (int)min((int64_t)a.chunk, a.n - nbase);
+        if (lane < ncount) nperm = ORD ? (int64_t)a.perm[nbase + lane] : nbase + lane;
+        nstage = 2;
+      };
+      auto stage3 = [&]() {
+        if (lane < ncount) {
+          ng = {a.pts[3 * nperm], a.pts[3 * nperm + 1], a.pts[3 * nperm + 2]};
+          ni = nperm;
+        }
+        nstage = 3;
+      };
+      if (nstage == 0 && pptr >= pcount - 24) stage1();
+      else if (nstage == 1 && pptr >= pcount - 16) stage2();
+      else if (nstage == 2 && pptr >= pcount - 8) stage3();
+      // hand prepared points to the free lanes, preparing batches as needed
+      const bool wasfree = !active;
+      const int rank = __popcll(freem & lt_mask);
       int handed = 0;
       while (handed < nfree) {
-        if (qnext >= qend) {
+        if (pptr >= pcount) {
           IKHIP_DG(kDiagGrabs, 1);
-          unsigned long long old = 0;
-          if (lane == 0) old = atomicAdd(&a.S->queue, (unsigned long long)a.chunk);
-          old = __shfl(old, 0, 64);
-          if ((int64_t)old >= a.n) {
-            exhausted = true;
-            break;
+#ifdef IKHIP_DIAG
+          const unsigned long long tp0 = __builtin_amdgcn_s_memrealtime();
+#endif
+          if (nstage == 0) stage1();
+          if (nstage == 1) stage2();
+          if (nstage == 2) stage3();
+          if (nstage < 0) break;
+          // prepare: limits check and seed pose of the batch, one entry per lane
+          pcount = ncount;
+          pptr = 0;
+          nstage = 0;
+          if (lane < pcount) {
+            const RcConst k = opaque_rc(a.rc);
+            if (a.check_limits && outside_rc(k, ng))
+              atomicMin(&a.S->first_oob, (unsigned long long)ni);
+            d3 Js[4];
+#ifndef IKHIP_EXP_NOSEED
+            (void)seed_pose((const RobotConstDev *)k, ng, Js);
+#else
+            Js[0] = {0.0, 0.0, 2.0}; Js[1] = {ng.x * 0.1, ng.y * 0.1, 4.0}; Js[2] = {ng.x * 0.2, ng.y * 0.2, 6.0};
+#endif
+            P0 = Js[0];
+            P1 = Js[1];
+            P2 = Js[2];
+            Pg = ng;
+            Pidx = ni;
           }
-          qnext = (int64_t)old;
-          qend = min((int64_t)old + a.chunk, a.n);
+#ifdef IKHIP_DIAG
+          // (the seed's loads are consumed before the stamp)
+          asm volatile("" ::"v"(P0.x), "v"(P1.x), "v"(P2.x), "v"(Pg.x));
+          dg[kDiagPrepTicks] += __builtin_amdgcn_s_memrealtime() - tp0;
+#endif
         }
-        int take = (int)min((int64_t)(nfree - handed), qend - qnext);
-        if (!active && rank >= handed && rank < handed + take) mine = qnext + (rank - handed);
-        qnext += take;
+        const int take = min(nfree - handed, pcount - pptr);
+        const bool mine = wasfree && rank >= handed && rank < handed + take;
+        const int src = mine ? pptr + (rank - handed) : lane;
+        const d3 n0 = shfl3(P0, src), n1 = shfl3(P1, src), n2 = shfl3(P2, src);
+        const d3 gq = shfl3(Pg, src);
+        const int64_t iq = __shfl(Pidx, src, 64);
+        if (mine) {
+          J0 = n0;
+          J1 = n1;
+          J2 = n2;
+          g = gq;
+          out = iq;
+          st = IK_OK;
+          se = 1.0;
+          ge = 1.0;
+          step = 0;
+          active = true;
+          if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
+        }
+        pptr += take;
         handed += take;
       }
-      if (mine >= 0) {
-        idx = mine;
-        d3 Jn[4];
-        if constexpr (ORD) {
-          const int64_t p = a.perm[idx];
-          st = a.status_in[p];
-          load_joints(a.seeds, p, Jn);
-          g = {a.pts[3 * p], a.pts[3 * p + 1], a.pts[3 * p + 2]};
-          out = p;
-        } else {
-          st = a.status[idx];
-          load_joints(a.seeds, idx, Jn);
-          g = {a.pts[3 * idx], a.pts[3 * idx + 1], a.pts[3 * idx + 2]};
-          out = idx;
-        }
-        // consume the gathered operands here: left pending, their loads made the
-        // compiler put an s_waitcnt vmcnt(0) at the top of every step (the join
-        // of the refill and no-refill paths), which also waited out the result
-        // stores of the lanes that finished the step before
-        asm volatile("" ::"v"(st), "v"(Jn[0].x), "v"(Jn[0].y), "v"(Jn[0].z), "v"(Jn[1].x),
-                     "v"(Jn[1].y), "v"(Jn[1].z), "v"(Jn[2].x), "v"(Jn[2].y), "v"(Jn[2].z));
-        asm volatile("" ::"v"(Jn[3].x), "v"(Jn[3].y), "v"(Jn[3].z), "v"(g.x), "v"(g.y),
-                     "v"(g.z));
-        J0 = Jn[0]; J1 = Jn[1]; J2 = Jn[2]; J3 = Jn[3];
-        if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
-        se = 1.0;
-        ge = 1.0;
-        step = 0;
-        active = true;
-      }
+      dry = nstage < 0 && pptr >= pcount;
     }
 #ifdef IKHIP_DIAG
     {
@@ -572,7 +719,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
           __ballot(active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step));
       dg[kDiagSteps] += sm ? 1 : 0;
       dg[kDiagLaneSteps] += __popcll(sm);
-      if (exhausted) {
+      if (nstage < 0) {
         if (!t_dry) t_dry = __builtin_amdgcn_s_memrealtime();
         steps_dry += sm ? 1 : 0;
       }
@@ -618,13 +765,29 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
         }
         ++step;
       } else {
-        d3 J[4] = {J0, J1, J2, J3};
-        store_joints(a.joints, out, J);
-        a.iters[out] = step;
-        a.status[out] = (uint8_t)st;
         active = false;
+        pending = true;
       }
     }
+  }
+  // drain: park the last finished lanes, then the angles step on the ring
+  {
+    const unsigned long long pm = __ballot(pending);
+    const int np = __popcll(pm);
+    if (rcnt + np > 64) {
+      ring_flush<ORD>(a, R, rcnt, lane, acc);
+      rcnt = 0;
+    }
+    if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, out, step, st);
+    rcnt += np;
+    IKHIP_DG(kDiagFlushes, 1);
+#ifdef IKHIP_DIAG
+    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    ring_flush<ORD>(a, R, rcnt, lane, acc);
+#ifdef IKHIP_DIAG
+    dg[kDiagFlushTicks] += __builtin_amdgcn_s_memrealtime() - tf0;
+#endif
   }
 #ifdef IKHIP_DIAG
   if (a.dbg && lane == 0) {
@@ -640,55 +803,30 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   }
 #endif
 #undef IKHIP_DG
-}
-
-// 3. angles + stats (uniform work, one point per lane).  ORD: 1 in kOrdSample
-// points records (cell, iterations) for the next call's cost table.
-template <bool ORD>
-__global__ __launch_bounds__(256) void fabrik_angles_kernel(FabArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool valid = i < a.n;
-  int it = 0;
-  if (valid) {
-    int st = a.status[i];
-    it = a.iters[i];
-    d3 J[4];
-    double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
-    if (st == IK_OK) load_joints(a.joints, i, J);
-    if (st == IK_OK) get_angles(J, th, st);
-    if (st != IK_OK) record_error(a.S, i, st);
-    double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
-    o[0] = make_double2(th[0], th[1]);
-    o[1] = make_double2(th[2], th[3]);
-    if constexpr (ORD) {
-      if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
-        a.ord->sample[i / kOrdSample] =
-            ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) |
-            (uint32_t)(it < 0xffff ? it : 0xffff);
-    }
-  }
+  block_iter_stats_acc(a.S, acc.sum_it, acc.capped, acc.max_it);
+  if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
   if constexpr (ORD) {
-    if (i == 0) {
+    // the last block to finish folds this call's records into the cost table
+    // (the next call's classify reads it); every thread fences its sample stores
+    __shared__ int last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      last = atomicAdd(&a.S->ticket, 1ull) == (unsigned long long)(gridDim.x - 1);
+    __syncthreads();
+    if (last) {
+      __threadfence();
       const int64_t ns = (a.n + kOrdSample - 1) / kOrdSample;
-      a.ord->nsample = (uint32_t)(ns < kOrdMaxSample ? ns : kOrdMaxSample);
+      order_fold(a.ord, (unsigned int)(ns < kOrdMaxSample ? ns : kOrdMaxSample));
     }
-    if (i < (int64_t)kOrdClasses * a.nseg) a.ord->hist[i] = 0;  // for the next call
   }
-  block_iter_stats(a.S, valid, it, a.max_iter);
 }
 
 static size_t up256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t fabrik_scratch_bytes(int64_t n) {
-  // seeds n*12 doubles, joints n*12 doubles, iters n int32, status n bytes;
-  // work order: perm n int32, cell n uint16, seed status n bytes
-  size_t b = 0;
-  b += up256((size_t)n * 96);
-  b += up256((size_t)n * 96);
-  b += up256((size_t)n * 4);
-  b += up256((size_t)n);
-  b += up256((size_t)n * 4) + up256((size_t)n * 2) + up256((size_t)n);
-  return b + 1024;
+  // work order: perm n int32, cell n uint16
+  return up256((size_t)n * 4) + up256((size_t)n * 2) + 1024;
 }
 
 // CUs of the current device, cached per device index (relaxed atomics: every
@@ -723,8 +861,8 @@ static void launch_iter(int core, unsigned grid, hipStream_t stream, const FabAr
 
 void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double tol,
                          int max_iter, double *ang, int32_t *iters, double *joints,
-                         bool check_limits, void *scratch, DevStats *S, hipStream_t stream,
-                         int variant, int core_req, FabOrderDev *ord,
+                         double *fk_err, bool check_limits, void *scratch, DevStats *S,
+                         hipStream_t stream, int variant, int core_req, FabOrderDev *ord,
                          const RobotConstDev *rc, unsigned long long *dbg, int bpc_req) {
   if (n <= 0) return;
   FabArgs a;
@@ -740,62 +878,39 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   a.ang = ang;
   a.iters = iters;
   a.joints = joints;
+  a.fk_err = fk_err;
   a.S = S;
   a.chunk = 64;
   a.perm = nullptr;
-  a.status_in = nullptr;
   a.cell = nullptr;
   a.ord = ord;
-  a.nseg = 0;
-  a.seg_blocks = 1;
-  unsigned grid = (unsigned)((n + 255) / 256);
-  if (variant == 0) {
-    a.seeds = nullptr;
-    a.status = nullptr;
+  // the seed's own angles (robot_const_kernel's check, forward.py:23-25)
+  bool robot_ok = true;
+  for (int k = 1; k < 4; ++k)
+    if (r.dh[k] < -2 * kPi || r.dh[k] > 2 * kPi) robot_ok = false;
+  for (int k = 0; k < 4; ++k)
+    if (r.dh[12 + k] < -2 * kPi || r.dh[12 + k] > 2 * kPi) robot_ok = false;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  // no iteration at all when the loop's initial errors of 1.0 already pass
+  if (variant == 0 || max_iter <= 0 || !(1.0 > a.tol2) || !robot_ok) {
     kt_begin("fabrik_simple_kernel", stream);
     hipLaunchKernelGGL(fabrik_simple_kernel, dim3(grid), dim3(256), 0, stream, a);
     kt_end(stream);
     return;
   }
-  char *p = static_cast<char *>(scratch);
-  a.seeds = reinterpret_cast<double *>(p);
-  p += up256((size_t)n * 96);
-  double *jtmp = reinterpret_cast<double *>(p);
-  p += up256((size_t)n * 96);
-  int32_t *itmp = reinterpret_cast<int32_t *>(p);
-  p += up256((size_t)n * 4);
-  a.status = reinterpret_cast<uint8_t *>(p);
-  p += up256((size_t)n);
   static const int order_on = env_int("IKHIP_FABRIK_ORDER", 1);
   const bool ordered = ord && order_on && n < (int64_t)1 << 31;
   if (ordered) {
-    // the iteration kernel writes its results by point index (a lane keeps its
-    // point's index from the refill gather), straight into the caller's
-    // (nullable) iterations / joints buffers
+    char *p = static_cast<char *>(scratch);
     a.perm = reinterpret_cast<int32_t *>(p);
     p += up256((size_t)n * 4);
     a.cell = reinterpret_cast<uint16_t *>(p);
-    p += up256((size_t)n * 2);
-    a.status_in = reinterpret_cast<uint8_t *>(p);
-    a.seg_blocks = (int)((grid + kOrdMaxSeg - 1) / kOrdMaxSeg);
-    if (a.seg_blocks < kOrdSegBlocksMin) a.seg_blocks = kOrdSegBlocksMin;
-    a.nseg = (int)((grid + a.seg_blocks - 1) / a.seg_blocks);
-    if (!a.joints) a.joints = jtmp;
-    if (!a.iters) a.iters = itmp;
-    kt_begin("fabrik_seed_kernel", stream);
-    hipLaunchKernelGGL(fabrik_seed_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
+    const unsigned ogrid = (unsigned)((n + 256 * kOrdPPT - 1) / (256 * kOrdPPT));
+    kt_begin("fabrik_classify_kernel", stream);
+    hipLaunchKernelGGL(fabrik_classify_kernel, dim3(ogrid), dim3(256), 0, stream, a);
     kt_end(stream);
-    kt_begin("fabrik_order_scan_kernel", stream);
-    hipLaunchKernelGGL(fabrik_order_scan_kernel, dim3(1), dim3(256), 0, stream, ord, a.nseg);
-    kt_end(stream);
-    kt_begin("fabrik_order_scatter_kernel", stream);
-    hipLaunchKernelGGL(fabrik_order_scatter_kernel, dim3(grid), dim3(256), 0, stream, a);
-    kt_end(stream);
-  } else {
-    if (!a.joints) a.joints = jtmp;
-    if (!a.iters) a.iters = itmp;
-    kt_begin("fabrik_seed_kernel", stream);
-    hipLaunchKernelGGL(fabrik_seed_kernel<false>, dim3(grid), dim3(256), 0, stream, a);
+    kt_begin("fabrik_scatter_kernel", stream);
+    hipLaunchKernelGGL(fabrik_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
     kt_end(stream);
   }
   // persistent grid: blocks_per_cu 256-thread blocks per CU (= waves per SIMD)
@@ -804,15 +919,14 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   // = a longer divergent tail); 2 and 3 are within noise at 1-1.25M points, and
   // from 4M points on 3 wins by ~5 % at every tolerance (the tail matters less
   // than the latency a third wave per SIMD hides), and so it does at 1M points
-  // with tol 1e-5 (56 iterations per point against 33 at 1e-3: 0.559 vs 0.586 ms
-  // per launch with the reuse iteration; at 1e-3 2 stays ahead, 0.386 vs 0.395).
+  // with tol 1e-5 (56 iterations per point against 33 at 1e-3).
   // (4M / 10M points at tol 1e-3: 4 per CU is 2 % ahead of 3; at 1e-5 they are even)
   // bpc_req: the context's IKHIP_FABRIK_BPC (0 = this rule)
-  const int bpc = bpc_req > 0 ? bpc_req
-                              : (n >= 4000000 && tol >= 1e-4) ? 4
-                                                              : ((n >= 2000000 || tol < 1e-4) ? 3 : 2);
+  // The fused kernel keeps the batch of prepared points and the angles step's
+  // temporaries beside the loop state: ~250 VGPRs, two waves per SIMD at most.
+  const int bpc = bpc_req > 0 ? (bpc_req < 2 ? bpc_req : 2) : 2;
   static const int chunk = env_int("IKHIP_FABRIK_CHUNK", 64);
-  a.chunk = chunk > 0 ? chunk : 64;
+  a.chunk = (chunk > 0 && chunk <= 64) ? chunk : 64;
   unsigned pgrid = (unsigned)num_cus() * (unsigned)(bpc > 0 ? bpc : 8);
   int64_t waves_needed = (n + 63) / 64;
   if ((int64_t)pgrid * 4 > waves_needed)
@@ -837,13 +951,6 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     else launch_iter<8, false>(core, pgrid, stream, a);
   }
   kt_end(stream);
-  kt_begin("fabrik_angles_kernel", stream);
-  if (ordered)
-    hipLaunchKernelGGL(fabrik_angles_kernel<true>, dim3(grid), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL(fabrik_angles_kernel<false>, dim3(grid), dim3(256), 0, stream, a);
-  kt_end(stream);
-
 }
 
 // ------------------------------------------------------ Fabrik.calculate ----

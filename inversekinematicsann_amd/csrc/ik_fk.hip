@@ -15,7 +15,11 @@ __global__ void reset_stats_kernel(DevStats *S) {
     S->first_oob = ~0ull;
     S->first_err_key = ~0ull;
     S->queue = 0;
-    S->pad0 = 0;
+    S->ticket = 0;
+  }
+  for (int e = t; e < kOrdClasses * kOrdShards; e += blockDim.x) {
+    (&S->cls_tot[0][0])[e] = 0;
+    (&S->cls_cur[0][0])[e] = 0;
   }
   if (t < kStatShards) {
     S->sum_iters[t] = 0;

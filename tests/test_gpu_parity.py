@@ -80,6 +80,39 @@ def test_fabrik_ragged_sizes(ctx):
     assert ang.shape == (0, 4)
 
 
+def test_fabrik_fk_err_equals_standalone_fk(ctx):
+    """The --verbose round trip (cli.py:54-72) fused into the FABRIK launch equals
+    |FK(theta) - p| from the standalone FK kernel on the same angles (1e-12),
+    and its batch stats are the reductions of the per-point errors."""
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    pts = random_dist(20_000, seed=17)
+    pts[5] = (0.0, 0.0, 2.0)  # ZeroDivisionError: NaN error, left out of the stats
+    for tol, mi in ((1e-3, 100), (1e-5, 200)):
+        ang, it, err, st = ctx.fabrik_solve_fk(pts, tol, mi)
+        ang2, it2, _, _ = ctx.fabrik_solve(pts, tol, mi)
+        assert np.array_equal(ang, ang2, equal_nan=True) and np.array_equal(it, it2)
+        assert st.first_err == 5 and st.first_err_code == 3 and math.isnan(err[5])
+        ok = np.ones(len(pts), bool)
+        ok[5] = False
+        xyz, _, _ = ctx.fk(ang[ok])
+        ref = np.sqrt(((xyz - pts[ok]) ** 2).sum(axis=1))
+        assert np.abs(err[ok] - ref).max() <= 1e-12
+        assert st.max_fk_err == err[ok].max()
+        assert abs(st.sum_fk_err - err[ok].sum()) <= 1e-9 * max(1.0, err[ok].sum())
+
+
+def test_fabrik_zero_iteration_solves(ctx):
+    """tol >= 1 (the loop's initial errors of 1.0 pass) and max_iter = 0 return the
+    seed pose's angles with 0 iterations, as the reference does (fabrik.py:53-59)."""
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    pts = random_dist(3000, seed=21)
+    for tol, mi in ((1.0, 100), (5.0, 100), (1e-3, 0)):
+        ang, it, _, st = ctx.fabrik_solve(pts, tol, mi)
+        rang, rit, _, _ = O.fabrik_ikine(pts, tol, mi)
+        assert np.array_equal(it, rit) and not it.any()
+        assert np.abs(ang - rang).max() <= 1e-9
+
+
 def test_fabrik_edge_cases_and_errors(ctx):
     with open(os.path.join(GOLDEN, "fabrik_edge.json")) as f:
         d = json.load(f)

@@ -16,7 +16,7 @@ os.environ.setdefault("IKHIP_LIB", os.path.join(ROOT, "inversekinematicsann_amd"
 from inversekinematicsann_amd import _native  # noqa: E402
 from inversekinematicsann_amd.robot.position_generator import random_dist  # noqa: E402
 
-NAMES = ["loops", "steps", "lane_steps", "refills", "grabs", "fallbacks", "waves"]
+NAMES = ["loops", "steps", "lane_steps", "refills", "grabs", "fallbacks", "waves", "flushes", "flush_ticks", "prep_ticks"]
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 pts = torch.from_numpy(random_dist(n, seed=0)).cuda()
 ang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
@@ -37,6 +37,8 @@ for tol, mi in ((1e-3, 100), (1e-5, 200)):
     us = lambda v: np.percentile((v - t0) / 100.0, [0, 1, 10, 50, 90, 99, 100]).round(1).tolist()
     c["lane_eff"] = c["lane_steps"] / (64.0 * max(c["steps"], 1))
     c["sum_iters"] = int(it.sum().item())
+    c["flush_us_per_wave"] = c["flush_ticks"] / 100.0 / max(c["waves"], 1)
+    c["prep_us_per_wave"] = c["prep_ticks"] / 100.0 / max(c["waves"], 1)
     c["steps_per_refill"] = c["steps"] / max(c["refills"], 1)
     c["pct"] = [0, 1, 10, 50, 90, 99, 100]
     c["wave_start_us"] = us(t[:, 0])
