@@ -4,14 +4,21 @@ Default workload (BASELINE.json configs[1]): ANN MLP forward of the reference
 architecture (ann.py:46-56: 3 -> 12 x Dense(500, tanh) -> Dense(4)) over 1M
 random_dist points per GPU in fp32, with the FK round-trip error fused in the
 same launch.  `--method fabrik` measures configs[2] (FABRIK, tol 1e-3 /
-100 iterations, float64).  One step = one solve of the whole per-GPU batch with
+100 iterations, float64).  One step = one solve of the whole batch with
 inputs already resident in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--method ann|fabrik]
+                    [--total-points T] [--gather 0|1]
 
-N > 1 is launched one process per GPU (torch.distributed.run); the batch is
-sharded by point (weak scaling: each rank solves its own 1M points, no
-collective on the data path); the step time is the max over ranks.
+N > 1 is launched one process per GPU (torch.distributed.run).  Every rank
+holds the same global batch (random_dist, seed 0; seed 1 from 10M points) and
+calls the library's sharded solve (ik_*_solve_sharded): it solves its
+contiguous shard and ONE RCCL all-gather inside libikhip delivers every
+rank's rows plus a tail record of its stats, so the step ends
+with the whole batch on every rank.  Weak scaling by default (1M points per
+GPU); --total-points 10000000 is configs[3] (ANN) / configs[4] (FABRIK tol
+1e-5 / 200) as strong scaling.  torch.distributed (gloo) is only the control
+plane: the RCCL id exchange, the barriers, the max over ranks of the step time.
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -59,29 +66,32 @@ def parse():
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01", "pmc"),
                     help="committed PMC diagnosis summaries (pipe occupancy in the roofline)")
-    ap.add_argument("--gather", type=int, default=0,
-                    help="N>1: include the RCCL all_gather of every rank's angle rows in the "
-                         "timed step (delivers the whole batch to every rank)")
+    ap.add_argument("--gather", type=int, default=1,
+                    help="N>1: the sharded solve with the library's RCCL all-gather of every "
+                         "rank's rows and stats in the timed step (1); 0 = every rank solves its "
+                         "shard only, no collective (also the one-GPU N>1 rehearsal mode)")
+    ap.add_argument("--total-points", type=int, default=0,
+                    help="global batch sharded over the ranks (strong scaling; configs[3] / "
+                         "configs[4] are 10000000); 0 = --points per GPU (weak scaling)")
     return ap.parse_args()
 
 
 def dist_setup(args):
+    """One process per GPU.  torch.distributed (gloo, CPU) is the control plane
+    only; the data path is the library's RCCL communicator (dist.ShardedContext)."""
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one GPU per rank; IKHIP_DIST_BACKEND=gloo + more ranks than GPUs is only for
-    # rehearsing the N > 1 bookkeeping on a one-GPU box (ranks share device 0)
-    backend = os.environ.get("IKHIP_DIST_BACKEND", "nccl")
-    if backend != "nccl":
+    # IKHIP_DIST_BACKEND=gloo + more ranks than GPUs: rehearsing the N > 1
+    # bookkeeping on a one-GPU box (ranks share device 0; use --gather 0 there,
+    # RCCL takes one rank per GPU)
+    if os.environ.get("IKHIP_DIST_BACKEND", "rccl") == "gloo":
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if "WORLD_SIZE" in os.environ:  # launched by torch.distributed.run (any N)
         import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
     return world, rank, local
 
 
@@ -96,28 +106,38 @@ def barrier(world):
         dist.barrier()
 
 
+def _reduce(v: float, op) -> float:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
 def max_over_ranks(v: float, world: int) -> float:
     if not _dist_on():
         return v
-    import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return _reduce(v, dist.ReduceOp.MAX)
 
 
 def sum_over_ranks(v: float, world: int) -> float:
     if not _dist_on():
         return v
-    import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _reduce(v, dist.ReduceOp.SUM)
 
 
 def _pts(n: int) -> str:
     return f"{n // 1_000_000}M" if n % 1_000_000 == 0 else f"{n}"
+
+
+def _batch_words(job) -> str:
+    if job.world == 1:
+        return f"{_pts(job.total)} random_dist points"
+    how = ("sharded contiguously, one RCCL all-gather of rows + stats inside libikhip"
+           if job.sc is not None else "sharded contiguously, no collective")
+    return f"{_pts(job.total)} random_dist points over {job.world} GPUs ({how})"
 
 
 def load_traffic(path, kernel):
@@ -149,50 +169,74 @@ def load_pipe(path, kernel):
     return None
 
 
-def make_gather(dang, args, world):
-    """The optional delivery step: all_gather of the per-rank angle rows over
-    RCCL (inversekinematicsann_amd.dist.gather_rows), on the solve's stream."""
-    if not args.gather or world == 1:
-        return lambda: None
-    from inversekinematicsann_amd.dist import gather_rows
-    n_total = dang.shape[0] * world
+class Job:
+    """The global batch and this rank's part of it.  sc: the library's sharded
+    context (N > 1 with --gather 1), else None (this rank's shard only)."""
 
-    def gather():
-        gather_rows(dang, n_total)
+    def __init__(self, ctx, sc, pts, dpts, lo, hi, world):
+        self.ctx, self.sc, self.pts, self.dpts = ctx, sc, pts, dpts
+        self.lo, self.hi, self.world = lo, hi, world
+        self.total = dpts.shape[0]
+        self.n_local = hi - lo
+        self.n_out = self.total if sc is not None else self.n_local  # rows a step returns
 
-    return gather
+    @property
+    def local_pts(self):
+        return self.dpts[self.lo:self.hi]
 
 
-def run_ann(ctx, dpts, n, args, world, mode="fp32"):
+def _stats_over_ranks(job, st, res):
+    """The batch's stats: already batch-wide after a sharded call (the gathered
+    tails), else each rank's shard reduced over the ranks."""
+    if job.sc is not None:
+        return st.max_fk_err, st.sum_fk_err, st.sum_iters, st.n_capped
+    w = job.world
+    return (max_over_ranks(st.max_fk_err, w), sum_over_ranks(st.sum_fk_err, w),
+            sum_over_ranks(st.sum_iters, w), sum_over_ranks(st.n_capped, w))
+
+
+def _p99(derr, world):
+    import torch
+    fin = derr[:1 << 24]
+    fin = fin[torch.isfinite(fin)]
+    return max_over_ranks(float(torch.quantile(fin, 0.99)) if fin.numel() else 0.0, world)
+
+
+def run_ann(job, args, mode="fp32"):
     import torch
     from inversekinematicsann_amd import _native
     from inversekinematicsann_amd.kinematics.ann import (REFERENCE_X_SCALER as XS,
                                                          REFERENCE_Y_SCALER as YS, glorot_model)
+    ctx, world = job.ctx, job.world
     m = glorot_model(ANN_DIMS, seed=0)
     ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
     ctx.ann_set_mode(mode)
-    dang = torch.empty((n, 4), dtype=torch.float32, device="cuda")
-    derr = torch.empty(n, dtype=torch.float64, device="cuda")
+    dang = torch.empty((job.n_out, 4), dtype=torch.float32, device="cuda")
+    derr = torch.empty(job.n_out, dtype=torch.float64, device="cuda")
     flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
 
-    gather = make_gather(dang, args, world)
-
-    def step():
-        ctx.ann_solve_device(dpts, dang, derr, flags=flags)
-        gather()
+    if job.sc is not None:
+        def step():  # solve the shard + the library's one RCCL all-gather
+            job.sc.ann_device(job.dpts, dang, derr, flags=flags)
+    else:
+        def step():
+            ctx.ann_solve_device(job.local_pts, dang, derr, flags=flags)
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
-    res["max_fk_err"] = max_over_ranks(st.max_fk_err, world)
-    res["mean_fk_err"] = sum_over_ranks(st.sum_fk_err, world) / (n * world)
-    res["p99_fk_err"] = max_over_ranks(float(torch.quantile(derr[:1 << 24], 0.99)), world)
+    mx, sm, _, _ = _stats_over_ranks(job, st, res)
+    res["max_fk_err"] = mx
+    res["mean_fk_err"] = sm / job.total
+    res["p99_fk_err"] = _p99(derr, world)
     res["outputs"] = {"ang": dang}
     res["end_to_end"] = end_to_end(
-        lambda hp: ctx.ann_solve(hp, check_limits=True, want_fk_err=True), dpts, args, world)
+        job, (lambda hp: job.sc.ann(hp, want_fk_err=True)) if job.sc is not None else
+        (lambda hp: ctx.ann_solve(hp, check_limits=True, want_fk_err=True)), args)
     ctx.ann_set_mode("fp32")
     flop_pt = m.flops_per_point()
     kname = "ann_fused_kernel" if mode == "fp32" else f"ann_fused_kernel_{mode}"
     k = res["kernels"].get(kname)
+    n = job.n_local
     achieved = flop_pt * n / (k / 1e3) if k else None
     # split modes: k bf16 / fp16 MFMA products per fp32 product, so the
     # fp32-equivalent matrix peak is the 16-bit peak / k (the input and output
@@ -212,7 +256,7 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
     if mode == "fp32":
         res["dtype"] = "fp32"
         res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
-                           f"{_pts(n)} random_dist points per GPU")
+                           + _batch_words(job))
     else:
         res["dtype"] = {"bf16x6": "fp32 via bf16x6 (3-way bf16 split, 6 MFMA products, fp32 "
                                   "accumulate)",
@@ -220,42 +264,48 @@ def run_ann(ctx, dpts, n, args, world, mode="fp32"):
                                   "operands, 3 MFMA products, fp32 accumulate)"}[mode]
         res["workload"] = (f"ANN MLP forward (3-12x500tanh-4), hidden GEMMs in the {mode} mode "
                            "(accuracy: tests/test_gpu_parity.py::test_ann_split_modes and "
-                           "cpu_baseline.parity) + fused FK round-trip error, "
-                           f"{_pts(n)} random_dist points per GPU")
+                           "cpu_baseline.parity) + fused FK round-trip error, " + _batch_words(job))
     return res
 
 
-def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
+def run_fabrik(job, args, tol=None, max_iter=None):
     import torch
     tol = args.tol if tol is None else tol
     max_iter = args.max_iter if max_iter is None else max_iter
     from inversekinematicsann_amd import _native
-    dang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
-    dit = torch.empty(n, dtype=torch.int32, device="cuda")
-    derr = torch.empty(n, dtype=torch.float64, device="cuda")
+    ctx, world = job.ctx, job.world
+    dang = torch.empty((job.n_out, 4), dtype=torch.float64, device="cuda")
+    dit = torch.empty(job.n_out, dtype=torch.int32, device="cuda")
+    derr = torch.empty(job.n_out, dtype=torch.float64, device="cuda")
     flags = _native.IK_F_DEVICE | _native.IK_F_ASYNC
 
-    gather = make_gather(dang, args, world)
-
-    def step():
-        # the --verbose FK round trip (cli.py:54-72) in the same launch as the angles
-        ctx.fabrik_solve_device(dpts, dang, dit, None, tol, max_iter, flags=flags, fk_err=derr)
-        gather()
+    # the --verbose FK round trip (cli.py:54-72) in the same launch as the angles
+    if job.sc is not None:
+        def step():  # solve the shard + the library's one RCCL all-gather
+            job.sc.fabrik_device(job.dpts, dang, dit, derr, tol, max_iter, flags=flags)
+    else:
+        def step():
+            ctx.fabrik_solve_device(job.local_pts, dang, dit, None, tol, max_iter, flags=flags,
+                                    fk_err=derr)
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
-    res["mean_iters"] = st.sum_iters / n
-    res["n_capped"] = st.n_capped
-    res["max_fk_err"] = max_over_ranks(st.max_fk_err, world)
-    res["mean_fk_err"] = sum_over_ranks(st.sum_fk_err, world) / (n * world)
-    fin = derr[:1 << 24]
-    res["p99_fk_err"] = max_over_ranks(float(torch.quantile(fin[torch.isfinite(fin)], 0.99)),
-                                       world)
+    mx, sm, sum_iters, n_capped = _stats_over_ranks(job, st, res)
+    n = job.n_local
+    res["mean_iters"] = sum_iters / job.total
+    res["n_capped"] = int(n_capped)
+    res["max_fk_err"] = mx
+    res["mean_fk_err"] = sm / job.total
+    res["p99_fk_err"] = _p99(derr, world)
     res["outputs"] = {"ang": dang, "iters": dit}
     res["end_to_end"] = end_to_end(
-        lambda hp: ctx.fabrik_solve(hp, tol, max_iter), dpts, args, world)
+        job, (lambda hp: job.sc.fabrik(hp, tol, max_iter)) if job.sc is not None else
+        (lambda hp: ctx.fabrik_solve(hp, tol, max_iter)), args)
+    # this rank's own iterations (the kernel's work), from its shard of the rows
+    own = dit[job.lo:job.hi] if job.sc is not None else dit
+    local_iters = int(own.sum().item())
     k = res["kernels"].get("fabrik_iter_kernel")
-    flops = FABRIK_FLOP_PER_ITER * st.sum_iters
+    flops = FABRIK_FLOP_PER_ITER * local_iters
     achieved = flops / (k / 1e3) if k else None
     traffic = load_traffic(args.traffic_file, "fabrik_iter_kernel")
     res["roofline"] = {"bound": "valu_fp64", "achieved": achieved / 1e12 if achieved else None,
@@ -263,7 +313,7 @@ def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
                        "frac": achieved / FP64_VALU_PEAK if achieved else None,
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
-                       "iterations_per_launch": int(st.sum_iters),
+                       "iterations_per_launch": local_iters,
                        # the flop count prices a correctly rounded sqrt / division as
                        # one flop; the pipes say how busy the SIMDs actually are
                        "pipes": load_pipe(os.path.join(args.pmc_dir,
@@ -271,20 +321,21 @@ def run_fabrik(ctx, dpts, n, args, world, tol=None, max_iter=None):
                                           "fabrik_iter_kernel")}
     res["dtype"] = "f64"
     res["workload"] = (f"FABRIK ikine (seed FK + loop + angles) + fused FK round-trip error, "
-                       f"tol {tol:g} / "
-                       f"{max_iter} iterations, float64, {_pts(n)} random_dist points per GPU")
+                       f"tol {tol:g} / {max_iter} iterations, float64, " + _batch_words(job))
     return res
 
 
 FK_BYTES_PER_POINT = 32 + 24   # float64 angles in, float64 effector xyz out
 
 
-def run_fk(ctx, dpts, n, args, world):
-    """Batched FK (forward.py:73-94, the DH chain) on n angle
-    vectors drawn uniformly in [-pi, pi): its bound is HBM (56 B per point) or
-    the float64 sin/cos + products, whichever is longer."""
+def run_fk(job, args):
+    """Batched FK (forward.py:73-94, the DH chain) on as many angle
+    vectors as this rank's shard has points, drawn uniformly in [-pi, pi): its
+    bound is HBM (56 B per point) or the float64 sin/cos + products, whichever is
+    longer.  No collective (each rank its own vectors)."""
     import torch
     from inversekinematicsann_amd import _native
+    ctx, world, n = job.ctx, job.world, job.n_local
     g = torch.Generator(device="cuda")
     g.manual_seed(7)
     dang = (torch.rand((n, 4), generator=g, dtype=torch.float64, device="cuda") * 2 - 1) * math.pi
@@ -308,6 +359,7 @@ def run_fk(ctx, dpts, n, args, world):
     res["dtype"] = "f64"
     res["unit"] = "FK evaluations/s"
     res["workload"] = f"FK (DH chain, float64), {_pts(n)} angle vectors per GPU"
+    res["total"] = n * world
     return res
 
 
@@ -343,23 +395,24 @@ def timed(ctx, step, args, world):
             "kernels": kernels}
 
 
-def end_to_end(solve_host, dpts, args, world):
+def end_to_end(job, solve_host, args):
     """PCIe-inclusive rate (SURVEY 8(d) "end-to-end"): host float64 points in,
     host angles out through the library's host-pointer path (H2D, kernels,
-    D2H, stats), pageable numpy buffers.  Reported beside `value`, never as it."""
+    D2H, stats; with N > 1 the sharded call and its all-gather), pageable numpy
+    buffers.  Reported beside `value`, never as it."""
     import torch
-    pts = dpts.cpu().numpy()
+    pts = job.pts if job.sc is not None else job.pts[job.lo:job.hi]
     reps = max(1, min(args.steps, 3))
     solve_host(pts)  # warm the staging scratch
-    barrier(world)
+    barrier(job.world)
     t0 = time.perf_counter()
     for _ in range(reps):
         solve_host(pts)
     torch.cuda.synchronize()
-    barrier(world)
-    wall = max_over_ranks(time.perf_counter() - t0, world)
+    barrier(job.world)
+    wall = max_over_ranks(time.perf_counter() - t0, job.world)
     ms = wall * 1e3 / reps
-    return {"ms_per_step": ms, "value": pts.shape[0] * world / (ms / 1e3), "steps": reps,
+    return {"ms_per_step": ms, "value": job.total / (ms / 1e3), "steps": reps,
             "unit": "IK solutions/s", "path": "host pointers (ik_*_solve without IK_F_DEVICE)"}
 
 
@@ -465,6 +518,20 @@ def cpu_baseline(method, args, sample_pts=None, gpu_out=None):
     return res
 
 
+def _config_ref(method, total, world, tol, max_iter):
+    """Which BASELINE.json config a line measures (configs[0] is the CPU plumbing)."""
+    if method == "ann":
+        if total >= 10_000_000 and world > 1:
+            return "configs[3]"
+        return "configs[1]" if total == 1_000_000 * world else None
+    if method == "fabrik":
+        if (tol, max_iter) == (1e-5, 200) and total >= 10_000_000 and world > 1:
+            return "configs[4]"
+        return "configs[2]" if (tol, max_iter) == (1e-3, 100) and total == 1_000_000 * world \
+            else None
+    return None
+
+
 def main():
     args = parse()
     import torch
@@ -472,23 +539,31 @@ def main():
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd import dist as D
     from inversekinematicsann_amd.robot.position_generator import random_dist
-    n = args.points
-    pts = random_dist(n, seed=rank)  # rank r solves shard r of the N x 1M global batch
+    strong = args.total_points > 0
+    total = args.total_points if strong else args.points * world
+    # the global batch, identical on every rank (seed 0; seed 1 from 10M)
+    pts = random_dist(total, seed=1 if total >= 10_000_000 else 0)
     dpts = torch.from_numpy(pts).cuda()
+    lo, hi = D.shard_bounds(total, world, rank)
     ctx = _native.Context(local)
-    # one non-default stream shared by the library, torch events and collectives
+    # one non-default stream shared by the library and torch's events
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
+    sc = None
+    if world > 1 and args.gather:
+        sc = D.ShardedContext(ctx, world, rank, D.exchange_unique_id(rank, D.torch_broadcast))
+    job = Job(ctx, sc, pts, dpts, lo, hi, world)
     other_modes = [m for m in ("fp32", "bf16x6", "fp16x3") if m != args.ann_mode]
-    runners = {"ann": lambda *a: run_ann(*a, mode=args.ann_mode), "fabrik": run_fabrik,
-               # configs[4]'s divergent-iteration stress settings on the per-GPU batch
-               "fabrik_tol1e-5": lambda *a: run_fabrik(*a, tol=1e-5, max_iter=200),
+    runners = {"ann": lambda j, a: run_ann(j, a, mode=args.ann_mode), "fabrik": run_fabrik,
+               # configs[4]'s divergent-iteration stress settings on the same batch
+               "fabrik_tol1e-5": lambda j, a: run_fabrik(j, a, tol=1e-5, max_iter=200),
                "fk": run_fk}
     for om in other_modes:
-        runners[f"ann_{om}"] = (lambda mm: lambda *a: run_ann(*a, mode=mm))(om)
-    res = runners[args.method](ctx, dpts, n, args, world)
+        runners[f"ann_{om}"] = (lambda mm: lambda j, a: run_ann(j, a, mode=mm))(om)
+    res = runners[args.method](job, args)
     outputs = {args.method: res["outputs"]}
     secondary = {}
     if args.secondary and args.method != "fk":
@@ -497,29 +572,41 @@ def main():
         if args.method == "fabrik" and (args.tol, args.max_iter) == (1e-5, 200):
             others.remove("fabrik_tol1e-5")
         for other in others:
-            r2 = runners[other](ctx, dpts, n, args, world)
-            secondary[other] = {"value": n * world / (r2["ms_per_step"] / 1e3),
+            r2 = runners[other](job, args)
+            secondary[other] = {"value": r2.get("total", total) / (r2["ms_per_step"] / 1e3),
                                 "unit": r2.get("unit", "IK solutions/s"),
                                 "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
                                 "roofline": r2["roofline"], "workload": r2["workload"],
+                                "kernels_ms": r2["kernels"],
                                 **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
                                                       "mean_iters", "n_capped", "end_to_end")
                                    if k in r2}}
+            cref = _config_ref("fabrik" if other.startswith("fabrik") else other, total, world,
+                               1e-5 if other == "fabrik_tol1e-5" else args.tol,
+                               200 if other == "fabrik_tol1e-5" else args.max_iter)
+            if cref:
+                secondary[other]["baseline_config"] = cref
             outputs[other] = r2["outputs"]
-    total = n * world
-    value = total / (res["ms_per_step"] / 1e3)
+    value = res.get("total", total) / (res["ms_per_step"] / 1e3)
     line = {
         "metric": METRIC, "value": value, "unit": res.get("unit", "IK solutions/s"), "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": res["ms_per_step"],
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": "strong" if strong else "weak", "vs_baseline": None,
         "dtype": res["dtype"],
-        "data": "synthetic: random_dist points (truncated normal sd 0.5 in the workspace box, "
-                "seed = rank); ANN weights random Glorot-uniform of the reference architecture "
-                "(the reference .h5 is not shipped); reference StandardScaler constants",
-        "config": {"workload": res["workload"], "points_per_gpu": n, "total_points": total,
+        "data": "synthetic: random_dist points (truncated normal sd 0.5 in the workspace box; "
+                "one global batch, seed 0, seed 1 from 10M points); ANN weights random "
+                "Glorot-uniform of the reference architecture (the reference .h5 is not "
+                "shipped); reference StandardScaler constants",
+        "config": {"workload": res["workload"],
+                   "baseline_config": _config_ref(args.method, total, world, args.tol,
+                                                  args.max_iter),
+                   "points_per_gpu": hi - lo, "total_points": total,
                    "parallelism": f"dp{world}", "method": args.method,
                    "ann_mode": args.ann_mode if args.method == "ann" else None,
-                   "all_gather_in_step": bool(args.gather and world > 1),
+                   "all_gather_in_step": sc is not None,
+                   "collective": ("one RCCL all-gather per step inside libikhip "
+                                  "(ik_*_solve_sharded): rows + per-rank stats tail")
+                   if sc is not None else None,
                    "tol": args.tol if args.method == "fabrik" else None,
                    "max_iter": args.max_iter if args.method == "fabrik" else None},
         "roofline": res["roofline"],
@@ -554,6 +641,8 @@ def main():
                                            line.get("secondary", {}).values()]:
             if isinstance(v, dict):
                 v.pop("_ref", None)
+    if sc is not None:
+        sc.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if _dist_on():

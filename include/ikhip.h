@@ -37,7 +37,8 @@ typedef enum ik_status {
   IK_E_ANGLE_RANGE = 4,  /* OutOfRobotReachException, kinematics/forward.py:23-25 */
   IK_E_BADARG = 16,      /* invalid argument (shape/size/order of calls) */
   IK_E_HIP = 17,         /* HIP runtime failure (see ik_last_error) */
-  IK_E_NOMODEL = 18      /* ik_ann_solve before ik_ann_load */
+  IK_E_NOMODEL = 18,     /* ik_ann_solve before ik_ann_load */
+  IK_E_RCCL = 19         /* RCCL missing or a collective failed (see ik_last_error) */
 } ik_status;
 
 enum {
@@ -57,8 +58,9 @@ typedef struct ik_stats {
   int32_t max_iters;      /* FABRIK: max iterations over the batch */
   int64_t sum_iters;      /* FABRIK: total iterations */
   int64_t n_capped;       /* FABRIK: points that hit max_iter */
-  double max_fk_err;      /* ANN: max |FK(theta) - p|_2 over the batch (if requested) */
-  double sum_fk_err;      /* ANN: sum of |FK(theta) - p|_2 */
+  double max_fk_err;      /* max |FK(theta) - p|_2 over the batch (if requested) */
+  double sum_fk_err;      /* sum of |FK(theta) - p|_2 */
+  double gather_ms;       /* sharded calls: the RCCL all-gather's duration (HIP events), else 0 */
 } ik_stats;
 
 /* ---- context ----------------------------------------------------------- */
@@ -168,6 +170,65 @@ int ik_debug_read(ik_ctx *ctx, uint64_t *out, int max);
 /* After IK_F_ASYNC calls: wait for the stream and read the accumulated stats
  * of the last call. */
 int ik_stats_fetch(ik_ctx *ctx, ik_stats *stats);
+
+/* ---- multi-GPU: RCCL over xGMI ------------------------------
+ * The reference scales by competing consumers of one RabbitMQ queue
+ * (rpc_broker.py:55-68); here one process per GPU shares the batch instead.
+ * Every rank calls the sharded solve with the same whole batch (n points, host
+ * or device pointer); rank r solves rows [floor(r n / g), floor((r+1) n / g))
+ * (ik_shard_range) and ONE all-gather over RCCL delivers every rank's rows and a
+ * tail record of its batch stats (ik_shard_tail), so each rank returns the whole
+ * batch's angles and the whole batch's stats (first_oob / first_err are the
+ * lowest GLOBAL indices: the reference's sequential exception precedence).
+ * With a device pointer only the rank's own rows of pts are read.  RCCL is
+ * loaded at ik_comm_init (the process's librccl if already loaded -- torch
+ * ships one --, else librccl.so.1; IKHIP_RCCL_LIB overrides). */
+#define IK_COMM_ID_BYTES 128
+
+/* The stats of one rank's shard as gathered (64 bytes). */
+typedef struct ik_shard_tail {
+  int64_t first_oob, first_err; /* GLOBAL indices, -1 if none */
+  int32_t first_err_code, max_iters;
+  int64_t sum_iters, n_capped;
+  double max_fk_err, sum_fk_err;
+  int64_t rows; /* rows the rank solved */
+} ik_shard_tail;
+
+/* The per-rank block of the all-gather, bytes: the rank's rows of each output
+ * region (angles, then iterations / FK errors when gathered), padded to the
+ * largest shard, then the tail record. */
+typedef struct ik_gather_layout {
+  int64_t shard;        /* rows per block (the largest shard) */
+  int64_t block_bytes;  /* bytes per rank */
+  int32_t nregion;      /* 1..3 */
+  int32_t row_bytes[3]; /* bytes per row of each region */
+  int64_t offset[3];    /* byte offset of each region in the block */
+  int64_t tail_offset;  /* byte offset of the ik_shard_tail */
+} ik_gather_layout;
+
+enum { IK_METHOD_ANN = 0, IK_METHOD_FABRIK = 1 };
+
+/* One rank creates the id and hands it to the others (any transport). */
+int ik_comm_unique_id(uint8_t *id /* IK_COMM_ID_BYTES */);
+/* Collective over the nranks processes: binds the context to an RCCL
+ * communicator (one GPU per rank). */
+int ik_comm_init(ik_ctx *ctx, int nranks, int rank, const uint8_t *id);
+int ik_comm_destroy(ik_ctx *ctx);
+/* Host-only helpers of the protocol (no device needed). */
+int ik_shard_range(int64_t n, int nranks, int rank, int64_t *begin, int64_t *end);
+int ik_gather_layout_of(int method, int64_t n, int nranks, int with_iters, int with_fk_err,
+                        ik_gather_layout *out);
+int ik_tail_reduce(const ik_shard_tail *tails, int nranks, ik_stats *out);
+
+/* AnnInverseKinematics.ikine / ANN.predict (see ik_ann_solve) over the ranks:
+ * ang n x 4 float32 and fk_err (nullable) n float64 of the WHOLE batch. */
+int ik_ann_solve_sharded(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *fk_err,
+                         int flags, ik_stats *stats);
+/* FabrikInverseKinematics.ikine (see ik_fabrik_solve_fk) over the ranks: ang n x 4
+ * float64, iters (nullable) n int32, fk_err (nullable) n float64, whole batch. */
+int ik_fabrik_solve_sharded(ik_ctx *ctx, const double *pts, int64_t n, double tol,
+                            int32_t max_iter, double *ang, int32_t *iters, double *fk_err,
+                            int flags, ik_stats *stats);
 
 #ifdef __cplusplus
 }

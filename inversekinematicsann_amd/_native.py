@@ -22,7 +22,9 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("IKHIP_LIB") or os.path.join(_PKG, "libikhip.so")
 
 IK_OK, IK_E_OUT_OF_REACH, IK_E_DOMAIN, IK_E_ZERODIV, IK_E_ANGLE_RANGE = 0, 1, 2, 3, 4
-IK_E_BADARG, IK_E_HIP, IK_E_NOMODEL = 16, 17, 18
+IK_E_BADARG, IK_E_HIP, IK_E_NOMODEL, IK_E_RCCL = 16, 17, 18, 19
+IK_METHOD_ANN, IK_METHOD_FABRIK = 0, 1
+IK_COMM_ID_BYTES = 128
 IK_F_DEVICE, IK_F_ASYNC, IK_F_NO_LIMITS = 1, 2, 4
 ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
 
@@ -30,7 +32,10 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk",
                     "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
-                    "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode")
+                    "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode",
+                    "ik_comm_unique_id", "ik_comm_init", "ik_comm_destroy", "ik_shard_range",
+                    "ik_gather_layout_of", "ik_tail_reduce", "ik_ann_solve_sharded",
+                    "ik_fabrik_solve_sharded")
 ANN_MODES = {"fp32": 0, "bf16x6": 1, "fp16x3": 2}
 
 
@@ -48,10 +53,27 @@ class IkStats(ctypes.Structure):
     _fields_ = [("first_oob", ctypes.c_int64), ("first_err", ctypes.c_int64),
                 ("first_err_code", ctypes.c_int32), ("max_iters", ctypes.c_int32),
                 ("sum_iters", ctypes.c_int64), ("n_capped", ctypes.c_int64),
-                ("max_fk_err", ctypes.c_double), ("sum_fk_err", ctypes.c_double)]
+                ("max_fk_err", ctypes.c_double), ("sum_fk_err", ctypes.c_double),
+                ("gather_ms", ctypes.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class ShardTail(ctypes.Structure):
+    """ik_shard_tail: one rank's batch stats as gathered (64 bytes)."""
+    _fields_ = [("first_oob", ctypes.c_int64), ("first_err", ctypes.c_int64),
+                ("first_err_code", ctypes.c_int32), ("max_iters", ctypes.c_int32),
+                ("sum_iters", ctypes.c_int64), ("n_capped", ctypes.c_int64),
+                ("max_fk_err", ctypes.c_double), ("sum_fk_err", ctypes.c_double),
+                ("rows", ctypes.c_int64)]
+
+
+class GatherLayout(ctypes.Structure):
+    """ik_gather_layout: the per-rank block of the sharded solves' all-gather."""
+    _fields_ = [("shard", ctypes.c_int64), ("block_bytes", ctypes.c_int64),
+                ("nregion", ctypes.c_int32), ("row_bytes", ctypes.c_int32 * 3),
+                ("offset", ctypes.c_int64 * 3), ("tail_offset", ctypes.c_int64)]
 
 
 _lib = None
@@ -104,6 +126,17 @@ def load_library(path: str = LIB_PATH):
         L.ik_debug_read.argtypes = [vp, vp, ctypes.c_int]
         L.ik_ann_set_mode.argtypes = [vp, ctypes.c_int]
         L.ik_ann_get_mode.argtypes = [vp]
+        L.ik_comm_unique_id.argtypes = [vp]
+        L.ik_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        L.ik_comm_destroy.argtypes = [vp]
+        L.ik_shard_range.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64),
+                                     ctypes.POINTER(i64)]
+        L.ik_gather_layout_of.argtypes = [ctypes.c_int, i64, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.POINTER(GatherLayout)]
+        L.ik_tail_reduce.argtypes = [vp, ctypes.c_int, st]
+        L.ik_ann_solve_sharded.argtypes = [vp, dp, i64, dp, dp, ctypes.c_int, st]
+        L.ik_fabrik_solve_sharded.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp,
+                                              ctypes.c_int, st]
         _lib = L
         return L
 
@@ -324,6 +357,63 @@ class Context:
                                           ctypes.byref(s)))
         return s
 
+    # -- multi-GPU (RCCL over xGMI; include/ikhip.h "multi-GPU") -------------
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        """Collective over the ranks: binds this context to an RCCL communicator."""
+        if len(uid) != IK_COMM_ID_BYTES:
+            raise ValueError(f"unique id must be {IK_COMM_ID_BYTES} bytes")
+        buf = ctypes.create_string_buffer(bytes(uid), IK_COMM_ID_BYTES)
+        self._check(self.lib.ik_comm_init(self.handle, int(nranks), int(rank), buf))
+
+    def comm_destroy(self):
+        self._check(self.lib.ik_comm_destroy(self.handle))
+
+    def ann_solve_sharded(self, pts, check_limits=True, want_fk_err=False):
+        """Host arrays: every rank passes the whole batch and gets the whole batch's
+        angles (float32) and stats back; it solves only its own shard."""
+        s = IkStats()
+        p = _host(pts, np.float64, 3)
+        n = p.shape[0]
+        ang = np.empty((n, 4), np.float32)
+        err = np.empty(n, np.float64) if want_fk_err else None
+        flags = 0 if check_limits else IK_F_NO_LIMITS
+        self._check(self.lib.ik_ann_solve_sharded(self.handle, _ptr(p), n, _ptr(ang), _ptr(err),
+                                                  flags, ctypes.byref(s)))
+        return ang, err, s
+
+    def fabrik_solve_sharded(self, pts, tol=1e-3, max_iter=100, check_limits=True,
+                             want_fk_err=False):
+        s = IkStats()
+        p = _host(pts, np.float64, 3)
+        n = p.shape[0]
+        ang = np.empty((n, 4), np.float64)
+        it = np.empty(n, np.int32)
+        err = np.empty(n, np.float64) if want_fk_err else None
+        flags = 0 if check_limits else IK_F_NO_LIMITS
+        self._check(self.lib.ik_fabrik_solve_sharded(self.handle, _ptr(p), n, float(tol),
+                                                     int(max_iter), _ptr(ang), _ptr(it),
+                                                     _ptr(err), flags, ctypes.byref(s)))
+        return ang, it, err, s
+
+    def ann_solve_sharded_device(self, pts, ang, fk_err=None, flags: int = IK_F_DEVICE):
+        s = IkStats()
+        n = int(pts.shape[0])
+        self._check(self.lib.ik_ann_solve_sharded(
+            self.handle, self._dev(pts, "float64", (n, 3), "pts"), n,
+            self._dev(ang, "float32", (n, 4), "ang"), self._dev(fk_err, "float64", (n,), "fk_err"),
+            flags, ctypes.byref(s)))
+        return s
+
+    def fabrik_solve_sharded_device(self, pts, ang, iters=None, fk_err=None, tol=1e-3,
+                                    max_iter=100, flags: int = IK_F_DEVICE):
+        s = IkStats()
+        n = int(pts.shape[0])
+        self._check(self.lib.ik_fabrik_solve_sharded(
+            self.handle, self._dev(pts, "float64", (n, 3), "pts"), n, float(tol), int(max_iter),
+            self._dev(ang, "float64", (n, 4), "ang"), self._dev(iters, "int32", (n,), "iters"),
+            self._dev(fk_err, "float64", (n,), "fk_err"), flags, ctypes.byref(s)))
+        return s
+
     def set_timing(self, on: bool = True):
         self._check(self.lib.ik_ctx_set_timing(self.handle, 1 if on else 0))
 
@@ -361,6 +451,45 @@ class Context:
         s = IkStats()
         self._check(self.lib.ik_stats_fetch(self.handle, ctypes.byref(s)))
         return s
+
+
+def _host_check(rc: int):
+    if rc != IK_OK:
+        raise NativeError(rc, load_library().ik_last_error().decode())
+
+
+def comm_unique_id() -> bytes:
+    """ncclGetUniqueId through the library (one rank calls it and shares the bytes)."""
+    L = load_library()
+    buf = ctypes.create_string_buffer(IK_COMM_ID_BYTES)
+    _host_check(L.ik_comm_unique_id(buf))
+    return buf.raw
+
+
+def shard_range(n: int, nranks: int, rank: int):
+    """ik_shard_range (host only): rank's rows [begin, end) of an n-point batch."""
+    b, e = ctypes.c_int64(), ctypes.c_int64()
+    _host_check(load_library().ik_shard_range(int(n), int(nranks), int(rank), ctypes.byref(b),
+                                              ctypes.byref(e)))
+    return b.value, e.value
+
+
+def gather_layout(method: int, n: int, nranks: int, with_iters: bool = False,
+                  with_fk_err: bool = False) -> GatherLayout:
+    """ik_gather_layout_of (host only): the per-rank block of the all-gather."""
+    L = GatherLayout()
+    _host_check(load_library().ik_gather_layout_of(int(method), int(n), int(nranks),
+                                                   int(bool(with_iters)), int(bool(with_fk_err)),
+                                                   ctypes.byref(L)))
+    return L
+
+
+def tail_reduce(tails: Sequence[ShardTail]) -> IkStats:
+    """ik_tail_reduce (host only): the batch stats from every rank's tail."""
+    arr = (ShardTail * len(tails))(*tails)
+    s = IkStats()
+    _host_check(load_library().ik_tail_reduce(arr, len(tails), ctypes.byref(s)))
+    return s
 
 
 _default_ctx: Optional[Context] = None

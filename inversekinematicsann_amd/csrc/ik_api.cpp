@@ -15,7 +15,7 @@
 #include <string>
 #include <vector>
 
-#include "ik_common.h"
+#include "ik_internal.h"
 
 using namespace ikhip;
 
@@ -23,31 +23,11 @@ namespace {
 
 thread_local std::string g_last_error;
 
-int fail(int code, const std::string &msg) {
-  g_last_error = msg;
-  return code;
-}
-
-#define IK_HIP(call)                                                                 \
-  do {                                                                               \
-    hipError_t e_ = (call);                                                          \
-    if (e_ != hipSuccess)                                                            \
-      return fail(IK_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_));     \
-  } while (0)
-
 const double kDefaultDh[16] = {0.0, kPi / 2, 0.0, 0.0, 2.0, 0.0, 0.0, 0.0,
                                0.0, 2.0,     2.0, 2.0, kPi / 2, 0.0, 0.0, 0.0};
 const double kDefaultLinks[4] = {2.0, 2.0, 2.0, 2.0};
 const double kDefaultLimits[6] = {0.0, 6.0, -6.0, 6.0, -3.0, 6.0};
 
-constexpr int kMaxTimed = 16;
-struct KTimer {
-  bool on = false;
-  int n = 0;
-  hipEvent_t beg[kMaxTimed] = {};
-  hipEvent_t end[kMaxTimed] = {};
-  const char *name[kMaxTimed] = {};
-};
 thread_local KTimer *g_kt = nullptr;
 
 }  // namespace
@@ -65,40 +45,18 @@ void kt_end(hipStream_t st) {
 }
 }  // namespace ikhip
 
-struct ik_ctx {
-  int device = 0;
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-  DevStats *d_stats = nullptr;
-  DevStats *h_stats = nullptr;  // pinned
-  void *scratch = nullptr;
-  size_t scratch_bytes = 0;
-  RobotDev robot;
-  bool ann_loaded = false;
-  AnnModelDev ann;
-  void *ann_buf = nullptr;
-  const void *ann_wx[kAnnMaxLayers] = {};  // bf16x6 weight operand of each layer (or null)
-  const void *ann_wh[kAnnMaxLayers] = {};  // fp16x3 weight operand of each layer (or null)
-  float ann_hinv[kAnnMaxLayers] = {};      // fp16x3: 2^-(weight pre-scale exponent)
-  int ann_mode = IK_ANN_FP32;
-  int fabrik_variant = 1;
-  int fabrik_bpc = 0;   // IKHIP_FABRIK_BPC: iteration-kernel blocks per CU (0 = size rule)
-  int fabrik_core = 2;  // IKHIP_FABRIK_CORE: 2 core + reuse, 1 sqrt_core / div_core, 0 general
-  KTimer kt;
-  unsigned long long *dbg = nullptr;  // diagnostic stamp buffer (ik_ctx_set_debug)
-  FabOrderDev *fab_ord = nullptr;     // FABRIK work-order cost table (learned per robot)
-  RobotConstDev *rconst = nullptr;    // FABRIK seed-pose constants of the robot
-};
+namespace ikapi {
 
-namespace {
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
 
-struct KtScope {
-  explicit KtScope(ik_ctx *c) {
-    g_kt = &c->kt;
-    c->kt.n = 0;
-  }
-  ~KtScope() { g_kt = nullptr; }
-};
+KtScope::KtScope(ik_ctx *c) {
+  g_kt = &c->kt;
+  c->kt.n = 0;
+}
+KtScope::~KtScope() { g_kt = nullptr; }
 
 int ensure_scratch(ik_ctx *c, size_t bytes) {
   if (bytes <= c->scratch_bytes) return IK_OK;
@@ -118,6 +76,7 @@ int set_dev(ik_ctx *c) {
 }
 
 void stats_from_dev(const DevStats &d, ik_stats *s) {
+  std::memset(s, 0, sizeof(*s));
   s->first_oob = (d.first_oob == ~0ull) ? -1 : (int64_t)d.first_oob;
   if (d.first_err_key == ~0ull) {
     s->first_err = -1;
@@ -126,11 +85,6 @@ void stats_from_dev(const DevStats &d, ik_stats *s) {
     s->first_err = (int64_t)(d.first_err_key >> 8);
     s->first_err_code = (int32_t)(d.first_err_key & 0xff);
   }
-  s->max_iters = 0;
-  s->sum_iters = 0;
-  s->n_capped = 0;
-  s->max_fk_err = 0.0;
-  s->sum_fk_err = 0.0;
   for (int i = 0; i < kStatShards; ++i) {
     s->max_iters = d.max_iters[i] > s->max_iters ? d.max_iters[i] : s->max_iters;
     s->sum_iters += (int64_t)d.sum_iters[i];
@@ -143,6 +97,7 @@ void stats_from_dev(const DevStats &d, ik_stats *s) {
 }
 
 int finish(ik_ctx *c, int flags, ik_stats *stats) {
+  c->last_sharded = false;
   if (flags & IK_F_ASYNC) return IK_OK;
   IK_HIP(hipMemcpyAsync(c->h_stats, c->d_stats, sizeof(DevStats), hipMemcpyDeviceToHost,
                         c->stream));
@@ -151,24 +106,39 @@ int finish(ik_ctx *c, int flags, ik_stats *stats) {
   return IK_OK;
 }
 
-// Staging plan for host-pointer calls: inputs copied into scratch, outputs
-// produced in scratch and copied back.
-struct Stage {
-  ik_ctx *c;
-  bool dev;
-  size_t off = 0;
-  char *base = nullptr;
-  struct Out {
-    void *host;
-    void *devp;
-    size_t bytes;
-  };
-  std::vector<Out> outs;
-  Stage(ik_ctx *cc, bool d) : c(cc), dev(d) {}
-  static size_t up(size_t b) { return (b + 255) & ~(size_t)255; }
-};
+}  // namespace ikapi
 
-}  // namespace
+using namespace ikapi;
+
+namespace ikapi {
+
+// Device pointers only, on the context's stream: stats reset + the kernels.
+int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_iter, double *da,
+                  int32_t *di, double *dj, double *dfe, bool limits, void *work) {
+  launch_reset_stats(c->d_stats, c->stream);
+  launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj, dfe, limits, work,
+                      c->d_stats, c->stream, c->fabrik_variant, c->fabrik_core, c->fab_ord,
+                      c->rconst, c->dbg, c->fabrik_bpc);
+  IK_HIP(hipGetLastError());
+  return IK_OK;
+}
+
+int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bool limits) {
+  launch_reset_stats(c->d_stats, c->stream);
+  AnnModelDev m = c->ann;
+  m.xmode = c->ann_mode;
+  for (int l = 0; l < m.n_layers; ++l) {
+    m.wx[l] = c->ann_mode == IK_ANN_BF16X6   ? c->ann_wx[l]
+              : c->ann_mode == IK_ANN_FP16X3 ? c->ann_wh[l]
+                                             : nullptr;
+    m.xinv[l] = c->ann_hinv[l];
+  }
+  launch_ann(m, c->robot, dp, n, da, de, limits, c->d_stats, c->stream, c->dbg);
+  IK_HIP(hipGetLastError());
+  return IK_OK;
+}
+
+}  // namespace ikapi
 
 extern "C" {
 
@@ -233,6 +203,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->fab_ord) (void)hipFree(c->fab_ord);
   if (c->rconst) (void)hipFree(c->rconst);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
+  comm_release(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   for (int i = 0; i < kMaxTimed; ++i) {
     if (c->kt.beg[i]) (void)hipEventDestroy(c->kt.beg[i]);
@@ -338,6 +309,7 @@ int ik_stats_fetch(ik_ctx *c, ik_stats *stats) {
   if (!c) return fail(IK_E_BADARG, "ik_stats_fetch: NULL context");
   int rc = set_dev(c);
   if (rc) return rc;
+  if (c->last_sharded) return sharded_stats(c, stats);
   return finish(c, 0, stats);
 }
 
@@ -435,12 +407,8 @@ int ik_fabrik_solve_fk(ik_ctx *c, const double *pts, int64_t n, double tol, int3
     q += b_jo;
     dfe = fk_err ? reinterpret_cast<double *>(q) : nullptr;
   }
-  launch_reset_stats(c->d_stats, c->stream);
-  launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj, dfe,
-                      !(flags & IK_F_NO_LIMITS), work, c->d_stats, c->stream,
-                      c->fabrik_variant, c->fabrik_core, c->fab_ord, c->rconst,
-                      c->dbg, c->fabrik_bpc);
-  IK_HIP(hipGetLastError());
+  rc = fabrik_launch(c, dp, n, tol, max_iter, da, di, dj, dfe, !(flags & IK_F_NO_LIMITS), work);
+  if (rc) return rc;
   if (!dev && n > 0) {
     IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 32, hipMemcpyDeviceToHost, c->stream));
     if (iters)
@@ -630,18 +598,8 @@ int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk
     da = reinterpret_cast<float *>(s + b_in);
     de = fk_err ? reinterpret_cast<double *>(s + b_in + b_a) : nullptr;
   }
-  launch_reset_stats(c->d_stats, c->stream);
-  AnnModelDev m = c->ann;
-  m.xmode = c->ann_mode;
-  for (int l = 0; l < m.n_layers; ++l) {
-    m.wx[l] = c->ann_mode == IK_ANN_BF16X6   ? c->ann_wx[l]
-              : c->ann_mode == IK_ANN_FP16X3 ? c->ann_wh[l]
-                                             : nullptr;
-    m.xinv[l] = c->ann_hinv[l];
-  }
-  launch_ann(m, c->robot, dp, n, da, de, !(flags & IK_F_NO_LIMITS), c->d_stats, c->stream,
-             c->dbg);
-  IK_HIP(hipGetLastError());
+  rc = ann_launch(c, dp, n, da, de, !(flags & IK_F_NO_LIMITS));
+  if (rc) return rc;
   if (!dev && n > 0) {
     IK_HIP(hipMemcpyAsync(ang, da, (size_t)n * 16, hipMemcpyDeviceToHost, c->stream));
     if (fk_err)

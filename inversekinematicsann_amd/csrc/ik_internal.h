@@ -1,0 +1,99 @@
+// ik_internal.h -- the context behind the C ABI and the helpers its
+// translation units share (ik_api.cpp: single-device calls; ik_comm.cpp: the
+// RCCL-sharded calls).  Not installed; include/ikhip.h is the interface.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "ik_common.h"
+
+namespace ikhip {
+constexpr int kMaxTimed = 16;
+struct KTimer {
+  bool on = false;
+  int n = 0;
+  hipEvent_t beg[kMaxTimed] = {};
+  hipEvent_t end[kMaxTimed] = {};
+  const char *name[kMaxTimed] = {};
+};
+}  // namespace ikhip
+
+// One RCCL communicator of a context (ik_comm_init): the buffers of the one
+// all-gather per sharded solve, grow-only like the scratch.
+struct IkComm {
+  void *comm = nullptr;  // ncclComm_t
+  int nranks = 0, rank = -1;
+  void *send = nullptr, *recv = nullptr;  // device: this rank's block, all blocks
+  size_t send_bytes = 0, recv_bytes = 0;
+  ik_shard_tail *h_tails = nullptr;  // pinned: every rank's tail record
+  int h_tails_n = 0;
+  hipEvent_t g0 = nullptr, g1 = nullptr;  // around the all-gather
+};
+
+struct ik_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  ikhip::DevStats *d_stats = nullptr;
+  ikhip::DevStats *h_stats = nullptr;  // pinned
+  void *scratch = nullptr;
+  size_t scratch_bytes = 0;
+  ikhip::RobotDev robot;
+  bool ann_loaded = false;
+  ikhip::AnnModelDev ann;
+  void *ann_buf = nullptr;
+  const void *ann_wx[ikhip::kAnnMaxLayers] = {};  // bf16x6 weight operand of each layer
+  const void *ann_wh[ikhip::kAnnMaxLayers] = {};  // fp16x3 weight operand of each layer
+  float ann_hinv[ikhip::kAnnMaxLayers] = {};      // fp16x3: 2^-(weight pre-scale exponent)
+  int ann_mode = IK_ANN_FP32;
+  int fabrik_variant = 1;
+  int fabrik_bpc = 0;   // IKHIP_FABRIK_BPC: iteration-kernel blocks per CU (0 = size rule)
+  int fabrik_core = 2;  // IKHIP_FABRIK_CORE: 2 core + reuse, 1 sqrt_core / div_core, 0 general
+  ikhip::KTimer kt;
+  unsigned long long *dbg = nullptr;     // diagnostic stamp buffer (ik_ctx_set_debug)
+  ikhip::FabOrderDev *fab_ord = nullptr;  // FABRIK work-order cost table (learned per robot)
+  ikhip::RobotConstDev *rconst = nullptr;  // FABRIK seed-pose constants of the robot
+  IkComm comm;
+  bool last_sharded = false;  // the last call's stats are in comm.h_tails
+  // the gathered tails of the last sharded call (for IK_F_ASYNC + ik_stats_fetch)
+  int64_t last_n = 0;
+};
+
+namespace ikapi {
+
+int fail(int code, const std::string &msg);
+
+#define IK_HIP(call)                                                                 \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess)                                                            \
+      return ::ikapi::fail(IK_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+// Per-kernel HIP-event timing of the current call (ik_ctx_set_timing).
+struct KtScope {
+  explicit KtScope(ik_ctx *c);
+  ~KtScope();
+};
+
+struct Stage {
+  static size_t up(size_t b) { return (b + 255) & ~(size_t)255; }
+};
+
+int ensure_scratch(ik_ctx *c, size_t bytes);
+int set_dev(ik_ctx *c);
+void stats_from_dev(const ikhip::DevStats &d, ik_stats *s);
+int finish(ik_ctx *c, int flags, ik_stats *stats);
+// Device pointers only, on the context's stream: stats reset + the solve's kernels.
+// work: fabrik_scratch_bytes(n) of device memory.
+int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_iter, double *da,
+                  int32_t *di, double *dj, double *dfe, bool limits, void *work);
+int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bool limits);
+// The batch stats of the last sharded call, from the gathered tails (waits).
+int sharded_stats(ik_ctx *c, ik_stats *stats);
+void comm_release(ik_ctx *c);
+
+}  // namespace ikapi

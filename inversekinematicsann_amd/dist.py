@@ -1,123 +1,128 @@
-"""Multi-GPU batch sharding (one process per GPU, torch.distributed over RCCL).
+"""Multi-GPU batch sharding: one process per GPU, libikhip's own RCCL over xGMI.
 
 The reference "scales" by running competing-consumer RPC workers, one message
 at a time (rpc_broker.py:55-104, README.md:11).  Here every point is
-independent, so a batch is split into contiguous shards, one per rank
-(rank r owns [floor(r N / g), floor((r+1) N / g))), each rank solves its shard
-on its own GPU with no communication, and -- only when the caller wants the
-whole result on every rank -- one all_gather of the per-point result rows
-(padded to equal shard length) reassembles the batch over xGMI.  The
-per-batch error reduction (first out-of-reach / first failing index) rides on
-a tiny all_reduce so the reference's "lowest index raises" rule holds across
-shards.
+independent, so one batch is split into contiguous shards (rank r owns
+[floor(r N / g), floor((r+1) N / g)), ik_shard_range), each rank solves its
+shard on its own GPU, and ONE all-gather inside the library
+(ik_*_solve_sharded) delivers every rank's result rows plus a tail record of
+its stats, so every rank ends with the whole batch and the whole batch's stats
+(the lowest global failing index -- the reference's sequential exception
+precedence -- iteration sums, FK-error max/sum) without any other collective.
+
+torch.distributed is only the control plane here: it hands rank 0's RCCL
+unique id to the other ranks (and gives bench.py its barrier); the data path
+is the library's communicator, as a C-ABI caller without torch would use it
+(INTEGRATION.md).
+
+The host-side mirror of the gather protocol (pack_block / unpack_blocks, the
+library's layout and tail records) is what the library does on the device and
+in its host-pointer path; the CPU tests drive it over gloo with world size 2.
 """
 from __future__ import annotations
 
-from typing import Callable, Optional, Tuple
+import ctypes
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from . import _native
+
 
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
+    """Rank's rows [begin, end) of an n-point batch (= ik_shard_range)."""
     return (n * rank) // world, (n * (rank + 1)) // world
 
 
-def max_shard(n: int, world: int) -> int:
-    return max(shard_bounds(n, world, r)[1] - shard_bounds(n, world, r)[0] for r in range(world))
+def exchange_unique_id(rank: int, broadcast: Callable[[Optional[bytes]], bytes]) -> bytes:
+    """Rank 0 asks the library for an RCCL unique id; `broadcast` hands it to
+    every rank (any transport: torch.distributed, MPI, a file)."""
+    uid = _native.comm_unique_id() if rank == 0 else None
+    return broadcast(uid)
 
 
-def gather_rows(local, n_total: int, group=None):
-    """All-gather the row-blocks of every rank into the full (n_total, ...)
-    tensor on every rank.  `local` holds this rank's shard_bounds rows."""
-    import torch
+def torch_broadcast(uid: Optional[bytes]) -> bytes:
+    """exchange_unique_id's transport over an initialised torch.distributed group."""
     import torch.distributed as dist
-    world = dist.get_world_size(group)
-    m = max_shard(n_total, world)
-    pad = torch.zeros((m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    pad[: local.shape[0]] = local
-    out = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype,
-                      device=local.device)
-    dist.all_gather_into_tensor(out, pad, group=group)
-    parts = []
-    for r in range(world):
-        lo, hi = shard_bounds(n_total, world, r)
-        parts.append(out[r * m: r * m + (hi - lo)])
-    return torch.cat(parts, 0)
+    box = [uid]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
 
 
-def reduce_first_index(idx: int, group=None, device=None) -> int:
-    """Global minimum of per-rank 'first failing' indices (-1 = none)."""
-    import torch
-    import torch.distributed as dist
-    big = np.iinfo(np.int64).max
-    t = torch.tensor([big if idx < 0 else idx], dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
-    v = int(t.item())
-    return -1 if v == big else v
+class ShardedContext:
+    """A libikhip context bound to an RCCL communicator of `world` ranks.
+    ann / fabrik take the WHOLE batch on every rank (host numpy arrays, or
+    device tensors via the *_device methods) and return the whole batch's
+    results and stats."""
+
+    def __init__(self, ctx: _native.Context, world: int, rank: int, uid: bytes):
+        self.ctx = ctx
+        self.world = int(world)
+        self.rank = int(rank)
+        ctx.comm_init(self.world, self.rank, uid)
+
+    def close(self):
+        self.ctx.comm_destroy()
+
+    def ann(self, pts, check_limits=True, want_fk_err=False):
+        return self.ctx.ann_solve_sharded(pts, check_limits, want_fk_err)
+
+    def fabrik(self, pts, tol=1e-3, max_iter=100, check_limits=True, want_fk_err=False):
+        return self.ctx.fabrik_solve_sharded(pts, tol, max_iter, check_limits, want_fk_err)
+
+    def ann_device(self, pts, ang, fk_err=None, flags=_native.IK_F_DEVICE):
+        return self.ctx.ann_solve_sharded_device(pts, ang, fk_err, flags)
+
+    def fabrik_device(self, pts, ang, iters=None, fk_err=None, tol=1e-3, max_iter=100,
+                      flags=_native.IK_F_DEVICE):
+        return self.ctx.fabrik_solve_sharded_device(pts, ang, iters, fk_err, tol, max_iter, flags)
 
 
-def solve_sharded(points_global, solver: Callable, n_out: int, out_dtype, *, gather=True,
-                  group=None, device=None):
-    """Shard `points_global` (N x 3, identical on every rank) across the ranks,
-    run `solver(local_points) -> (local_out (n_local x n_out), first_oob_local,
-    first_err_local, err_code)` on this rank's shard and optionally all_gather
-    the rows.  Returns (out, first_oob, first_err, err_code) with global
-    indices; out is the full batch if gather else this rank's shard."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    n = int(points_global.shape[0])
-    lo, hi = shard_bounds(n, world, rank)
-    local_out, oob, err, code = solver(points_global[lo:hi])
-    oob_g = reduce_first_index(oob + lo if oob >= 0 else -1, group, device)
-    err_g = reduce_first_index(err + lo if err >= 0 else -1, group, device)
-    # the code of the globally first error travels with its owner
-    c = torch.tensor([code if (err >= 0 and err + lo == err_g) else 0], dtype=torch.int32,
-                     device=device)
-    dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
-    if not torch.is_tensor(local_out):
-        local_out = torch.as_tensor(local_out, device=device)
-    if gather:
-        out = gather_rows(local_out.to(out_dtype).reshape(hi - lo, n_out), n, group)
-    else:
-        out = local_out
-    return out, oob_g, err_g, int(c.item())
-
-
-def gpu_solver(method: str, ctx, tol: float = 1e-3, max_iter: int = 100,
-               check_limits: bool = True) -> Callable:
-    """A solver for solve_sharded backed by libikhip on this rank's GPU:
-    device tensors in, device tensors out, no host round trip."""
-    import torch
-    from . import _native
-
-    def run(local_pts):
-        n = local_pts.shape[0]
-        flags = _native.IK_F_DEVICE | (0 if check_limits else _native.IK_F_NO_LIMITS)
-        if method == "fabrik":
-            ang = torch.empty((n, 4), dtype=torch.float64, device=local_pts.device)
-            st = ctx.fabrik_solve_device(local_pts, ang, None, None, tol, max_iter, flags=flags)
-        else:
-            ang = torch.empty((n, 4), dtype=torch.float32, device=local_pts.device)
-            st = ctx.ann_solve_device(local_pts, ang, None, flags=flags)
-        return ang, st.first_oob, st.first_err, st.first_err_code
-
-    return run
-
-
-def init_from_env(backend: Optional[str] = None):
-    """torch.distributed init for torchrun-launched ranks (MASTER_ADDR etc.)."""
+def init_from_env(ctx: _native.Context) -> ShardedContext:
+    """For torchrun-launched ranks (RANK / WORLD_SIZE / MASTER_*): a gloo control
+    group for the id exchange, then the library's RCCL communicator."""
     import os
-    import torch
     import torch.distributed as dist
-    if dist.is_initialized():
-        return
-    if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        dist.init_process_group(backend)
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    uid = exchange_unique_id(rank, torch_broadcast)
+    return ShardedContext(ctx, world, rank, uid)
+
+
+# ---- host mirror of the gather protocol ------------------------------------------
+def pack_block(layout: _native.GatherLayout, regions: Sequence[np.ndarray],
+               tail: _native.ShardTail) -> np.ndarray:
+    """One rank's block of the all-gather (uint8): region q's rows at offset[q],
+    then the tail record, as the library lays it out in its send buffer."""
+    blk = np.zeros(layout.block_bytes, np.uint8)
+    for q, arr in enumerate(regions):
+        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
+        if raw.size > layout.shard * layout.row_bytes[q]:
+            raise ValueError(f"region {q}: {raw.size} bytes exceed the layout's shard")
+        blk[layout.offset[q]: layout.offset[q] + raw.size] = raw
+    tb = np.frombuffer(bytes(tail), np.uint8)
+    blk[layout.tail_offset: layout.tail_offset + tb.size] = tb
+    return blk
+
+
+def unpack_blocks(layout: _native.GatherLayout, blocks: np.ndarray, n: int,
+                  dtypes: Sequence[np.dtype], widths: Sequence[int]):
+    """Every rank's block (world x block_bytes uint8) -> each region's rows of the
+    whole batch in point order, and the tails (what the library's unpack kernel
+    and per-rank D2H copies do)."""
+    world = blocks.shape[0]
+    outs: List[np.ndarray] = [np.empty((n, w), dt) for dt, w in zip(dtypes, widths)]
+    tails = []
+    for r in range(world):
+        lo, hi = shard_bounds(n, world, r)
+        for q, out in enumerate(outs):
+            rb = layout.row_bytes[q]
+            raw = blocks[r, layout.offset[q]: layout.offset[q] + (hi - lo) * rb]
+            out[lo:hi] = raw.view(out.dtype).reshape(hi - lo, out.shape[1])
+        t = _native.ShardTail()
+        ctypes.memmove(ctypes.addressof(t),
+                       blocks[r, layout.tail_offset:].ctypes.data, ctypes.sizeof(t))
+        tails.append(t)
+    return outs, tails
