@@ -172,6 +172,11 @@ class Context:
                                     f"{self.lib.ik_last_error().decode()}")
         self.handle = h
         self.device = int(device)
+        # what ik_ctx_create installed (SixDOFRobot, robot/robot.py:38-42)
+        self._robot = (np.array([0.0, np.pi / 2, 0.0, 0.0, 2.0, 0.0, 0.0, 0.0,
+                                 0.0, 2.0, 2.0, 2.0, np.pi / 2, 0.0, 0.0, 0.0]),
+                       np.array([2.0, 2.0, 2.0, 2.0]), np.array([0.0, 6.0, -6.0, 6.0, -3.0, 6.0]))
+        self.robot_uploads = 0
 
     def close(self):
         if getattr(self, "handle", None):
@@ -192,11 +197,22 @@ class Context:
     def set_stream(self, stream_handle: Optional[int]):
         self._check(self.lib.ik_ctx_set_stream(self.handle, stream_handle))
 
-    def set_robot(self, dh, links, limits):
+    def set_robot(self, dh, links=None, limits=None) -> bool:
+        """Upload a robot (None keeps the context's links / limits).  Skipped when
+        nothing the device reads changes: dh[0][0] (theta_1) is not read there --
+        every solve takes the point's own azimuth -- so the reference's per-call
+        write of the last point's theta_1 into the table (inverse.py:125) costs no
+        upload.  Returns whether ik_set_robot was called."""
         dh = _host(dh, np.float64).reshape(16)
-        links = _host(links, np.float64).reshape(4)
-        limits = _host(limits, np.float64).reshape(6)
+        links = self._robot[1] if links is None else _host(links, np.float64).reshape(4)
+        limits = self._robot[2] if limits is None else _host(limits, np.float64).reshape(6)
+        if (np.array_equal(dh[1:], self._robot[0][1:]) and np.array_equal(links, self._robot[1])
+                and np.array_equal(limits, self._robot[2])):
+            return False
         self._check(self.lib.ik_set_robot(self.handle, _ptr(dh), _ptr(links), _ptr(limits)))
+        self._robot = (dh.copy(), links.copy(), limits.copy())
+        self.robot_uploads += 1
+        return True
 
     # -- solves ---------------------------------------------------------------
     def check_limits(self, pts) -> IkStats:

@@ -227,12 +227,19 @@ int ik_set_robot(ik_ctx *c, const double *dh, const double *links, const double 
   if (dh) std::memcpy(c->robot.dh, dh, sizeof(c->robot.dh));
   if (links) std::memcpy(c->robot.links, links, sizeof(c->robot.links));
   if (limits) std::memcpy(c->robot.lim, limits, sizeof(c->robot.lim));
-  // the FABRIK cost table describes one chain: forget it when the chain changes
-  if (std::memcmp(old.dh, c->robot.dh, sizeof(old.dh)) ||
-      std::memcmp(old.links, c->robot.links, sizeof(old.links))) {
+  // dh[0] (theta_1) is never read on the device: every solve takes the point's
+  // own azimuth (inverse.py:123-125 writes it into the table per point), so a
+  // drop-in caller re-sending the table with the last point's theta_1 changes
+  // nothing.  The FABRIK cost table describes one chain (dh[1..15], links):
+  // forget it only when that changes; the seed / limit constants follow any
+  // change of those or of the limits.
+  const bool chain = std::memcmp(old.dh + 1, c->robot.dh + 1, 15 * sizeof(double)) ||
+                     std::memcmp(old.links, c->robot.links, sizeof(old.links));
+  const bool lim = std::memcmp(old.lim, c->robot.lim, sizeof(old.lim)) != 0;
+  if (chain || lim) {
     int rc = set_dev(c);
     if (rc) return rc;
-    IK_HIP(hipMemsetAsync(c->fab_ord, 0, sizeof(FabOrderDev), c->stream));
+    if (chain) IK_HIP(hipMemsetAsync(c->fab_ord, 0, sizeof(FabOrderDev), c->stream));
     launch_robot_const(c->robot, c->rconst, c->stream);
     IK_HIP(hipGetLastError());
     // synchronous: later calls may run on another stream (ik_ctx_set_stream)

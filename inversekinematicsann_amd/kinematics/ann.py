@@ -89,6 +89,23 @@ def save_npz_model(path, model: DenseModel, xs: ScalerParams, ys: ScalerParams):
              y_mean=ys.mean, y_scale=ys.scale, **arrs)
 
 
+def as_features(position) -> np.ndarray:
+    """The n x 3 float64 batch ANN.predict scales (ann.py:73): a single point
+    (3,) is one row; any other width fails like the reference's StandardScaler
+    (sklearn's feature-count check), never by reinterpreting the numbers."""
+    pts = np.asarray(position, dtype=np.float64)
+    if pts.ndim == 1 and pts.shape[0] == 3:
+        pts = pts.reshape(1, 3)
+    if pts.ndim == 2 and pts.shape[0] == 0:
+        return np.empty((0, 3), np.float64)
+    if pts.ndim != 2:
+        raise ValueError(f"Expected 2D array, got {pts.ndim}D array instead")
+    if pts.shape[1] != 3:
+        raise ValueError(f"X has {pts.shape[1]} features, but StandardScaler is expecting 3 "
+                         "features as input.")
+    return np.ascontiguousarray(pts)
+
+
 class ANN:
     """ANN class implementing the neural-network IK approach (ann.py:18-25)."""
 
@@ -118,16 +135,17 @@ class ANN:
         if self.model is None:
             raise RuntimeError("no model loaded: call load_model() first")
         if self._uploaded_to is not ctx or getattr(ctx, "_ann_owner", None) is not self:
+            xm, xs = self.x_data_skaler.effective()
+            ym, ys = self.y_data_skaler.effective()
             ctx.ann_load(self.model.weights, self.model.biases, self.model.activations,
-                         self.x_data_skaler.mean, self.x_data_skaler.scale,
-                         self.y_data_skaler.mean, self.y_data_skaler.scale)
+                         xm, xs, ym, ys)
             self._uploaded_to = ctx
             ctx._ann_owner = self
         return ctx
 
     def predict(self, position):
         """Scale input, run the network, rescale output (ann.py:70-76); no limit check."""
-        pts = np.ascontiguousarray(np.asarray(position, dtype=np.float64).reshape(-1, 3))
+        pts = as_features(position)
         ang, _, _ = self._ctx().ann_solve(pts, check_limits=False)
         return ang
 
@@ -138,7 +156,7 @@ class ANN:
 
     def predict_with_fk_error(self, position):
         """(angles, |FK(angles) - p|_2 per point, stats) -- the cli.py:54-61 round trip."""
-        pts = np.ascontiguousarray(np.asarray(position, dtype=np.float64).reshape(-1, 3))
+        pts = as_features(position)
         ang, err, st = self._ctx().ann_solve(pts, check_limits=False, want_fk_err=True)
         return ang, err, st
 

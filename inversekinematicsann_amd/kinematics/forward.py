@@ -28,9 +28,10 @@ class ForwardKinematics:
             raise NotImplementedError('the HIP FK kernel implements 4-joint DH chains')
 
     def _ctx(self):
+        """The process context with this object's DH table; the link lengths and
+        workspace limits it holds (another object's) are left as they are."""
         ctx = _native.context()
-        ctx.set_robot(np.asarray(self.dh_matrix, np.float64), [2.0, 2.0, 2.0, 2.0],
-                      [0, 6, -6, 6, -3, 6])
+        ctx.set_robot(np.asarray(self.dh_matrix, np.float64))
         return ctx
 
     def fkine(self, angles):

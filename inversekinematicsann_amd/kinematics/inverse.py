@@ -23,7 +23,7 @@ import numpy as np
 
 from .. import _native
 from ..robot.robot import OutOfRobotReachException
-from .ann import ANN
+from .ann import ANN, as_features as as_ann_points
 from .forward import ForwardKinematics
 from .fabrik import Fabrik
 
@@ -46,9 +46,17 @@ def limits_array(workspace_limits) -> np.ndarray:
 
 
 def as_points(dest_points) -> np.ndarray:
+    """The n x 3 float64 batch of destination points.  Every point must be 3D,
+    as the reference's Point (point.py:12-14) requires; a wrong width raises its
+    ValueError instead of being reinterpreted as other points."""
     pts = np.asarray(dest_points, dtype=np.float64)
+    if pts.ndim == 2 and pts.shape[0] == 0:
+        return np.empty((0, 3), np.float64)
+    if pts.ndim == 1 and pts.shape[0] == 0:
+        return np.empty((0, 3), np.float64)
     if pts.ndim != 2 or pts.shape[1] != 3:
-        pts = pts.reshape(-1, 3)
+        bad = pts.shape[1:] if pts.ndim >= 2 else pts.shape
+        raise ValueError(f'3D Point input shape should be (3,) not {tuple(bad)}')
     return np.ascontiguousarray(pts)
 
 
@@ -63,6 +71,10 @@ class InverseKinematics(ABC):
         self.last_stats = None
 
     def _ctx(self):
+        """The process context holding this object's robot: uploaded when it
+        differs from what the context holds (Context.set_robot compares), so
+        objects with different robots can interleave and repeated calls of one
+        object upload nothing."""
         ctx = _native.context()
         ctx.set_robot(np.asarray(self.dh_matrix, np.float64),
                       np.asarray(self.joints_distances, np.float64),
@@ -131,7 +143,7 @@ class AnnInverseKinematics(InverseKinematics):
 
     def ikine(self, dest_points):
         """Predicted joint angles (float32 values as Python floats)."""
-        pts = as_points(dest_points)
+        pts = as_ann_points(dest_points)
         if pts.shape[0] == 0:
             return []
         self._ctx()

@@ -40,6 +40,16 @@ class ScalerParams:
             X /= self.scale
         return X
 
+    def effective(self):
+        """(mean, scale) as the fused kernels apply them, (x - mean) / scale and
+        y * scale + mean: 0 / 1 where with_mean / with_std are off (sklearn
+        then skips the step; a fitted mean_ may still be set), which is exact."""
+        mean = np.asarray(self.mean, np.float64) if self.with_mean else np.zeros_like(
+            np.asarray(self.mean, np.float64))
+        scale = np.asarray(self.scale, np.float64) if self.with_std else np.ones_like(
+            np.asarray(self.scale, np.float64))
+        return mean, scale
+
     def inverse_transform(self, X):
         """StandardScaler.inverse_transform keeping a float32 input float32
         (numpy in-place ops with a float64 operand, rounded per op)."""

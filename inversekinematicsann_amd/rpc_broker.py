@@ -1,14 +1,17 @@
-"""RPC front-end -- the reference's rpc_broker.py JSON contract on the GPU engine.
+"""RPC service: batched IK requests over a RabbitMQ request/reply queue.
 
-SURVEY 8(f) rank 4.  The reference serves `{"positions": [[x, y, z], ...]}`
-requests from a RabbitMQ queue and answers `{"status": "OK", "angles": [...]}`
-or `{"status": "ERROR", "reason": str(e), "correlation_id": id}`
-(rpc_broker.py:70-100).  The payload logic is `IkineRequestHandler.handle`,
-transport-free and testable on its own; `IkineRPCBroker` is the same consumer
-(queue `ikine_queue` on host `rabbit_mq`, prefetch 1) and needs the `pika`
-client, which is optional: without it the broker refuses to start, the
-handler still works.  The engine is this package's `kinematics.inverse`
-classes, so every request is one batched GPU solve.
+The wire contract is the reference's (rpc_broker.py:57-104),
+kept byte-compatible with its clients (examples/rpc_client.py):
+
+    request  {"positions": [[x, y, z], ...]}
+    reply    {"status": "OK", "angles": [[t1, t2, t3, t4], ...]}
+          or {"status": "ERROR", "reason": "<exception text>", "correlation_id": <id>}
+
+on queue "ikine_queue" of host "rabbit_mq", one unacknowledged request at a
+time.  A request is one batched GPU solve through this package's
+kinematics.inverse engines.  `IkineRequestHandler` is the transport-free part
+(bytes in, bytes out); `IkineRPCBroker` binds it to RabbitMQ and needs the
+optional `pika` client.
 
     python -m inversekinematicsann_amd.rpc_broker --method fabrik
     python -m inversekinematicsann_amd.rpc_broker --method ann --model M.h5
@@ -17,8 +20,8 @@ from __future__ import annotations
 
 import argparse
 import json
-import os
-import sys
+import logging
+from typing import List, Optional, Sequence
 
 from inversekinematicsann_amd.kinematics.inverse import (AnnInverseKinematics,
                                                          FabrikInverseKinematics)
@@ -26,103 +29,117 @@ from inversekinematicsann_amd.kinematics.point import Point
 from inversekinematicsann_amd.robot.robot import OutOfRobotReachException
 from inversekinematicsann_amd.robot.robot import SixDOFRobot as Robot
 
-DEBUG_MSG = False
+RPC_HOST = "rabbit_mq"
+RPC_QUEUE = "ikine_queue"
+
+# What a bad request can raise and the client gets back as an ERROR reply: a
+# point out of reach, a malformed body or point (json / Point), a non-list
+# "positions".  Anything else (a body without "positions", ZeroDivisionError at
+# the base-top joint) is a fault of the service and propagates, as it does in
+# the reference.
+REPLY_ERRORS = (OutOfRobotReachException, ValueError, TypeError)
+
+log = logging.getLogger("ikhip.rpc")
 
 
-def debug_msg_print(msg):
-    if DEBUG_MSG:
-        print(msg)
+def decode_request(body: bytes) -> List[Point]:
+    return [Point(p) for p in json.loads(body.decode())["positions"]]
 
 
-def get_ikine_engine_cli(argv=None):
-    """rpc_broker.py:26-54: `--method {ann,fabrik}` (+ `--model` for ann)."""
-    p = argparse.ArgumentParser(prog="cli")
-    p.add_argument("--method", required=True, type=str, choices=["ann", "fabrik"],
-                   help="select inverse kinematics method, Neural Network or Fabrik")
-    known, _ = p.parse_known_args(argv)
-    if known.method == "ann":
-        p.add_argument("--model", type=str, required=True,
-                       help="select .h5 file with saved model, required only if ann ikine "
-                            "method was choosed")
-    args = p.parse_args(argv)
-    if args.method == "ann":
-        engine = AnnInverseKinematics(Robot.dh_matrix, Robot.links_lengths,
-                                      Robot.effector_workspace_limits)
-        engine.load_model(args.model)
-        return engine
-    return FabrikInverseKinematics(Robot.dh_matrix, Robot.links_lengths,
-                                   Robot.effector_workspace_limits)
+def ok_reply(angles) -> dict:
+    return {"status": "OK", "angles": angles}
 
 
-def exception_response(status, reason, corr_id):
-    """rpc_broker.py:68-72."""
-    return {"status": status, "reason": reason, "correlation_id": corr_id}
+def error_reply(exc: BaseException, correlation_id) -> dict:
+    return {"status": "ERROR", "reason": str(exc), "correlation_id": correlation_id}
 
 
 class IkineRequestHandler:
-    """The body of the reference's callback (rpc_broker.py:74-92): request bytes
-    in, response bytes out.  OutOfRobotReachException, ValueError (including a
-    malformed JSON body or a point that is not 3 numbers) and TypeError become
-    an ERROR response; anything else (ZeroDivisionError at (0, 0, 2), a body
-    without "positions") propagates, as in the reference."""
+    """One request body -> one reply body, through an engine with ikine()."""
 
     def __init__(self, ikine):
         self.ikine = ikine
 
     def handle(self, body: bytes, correlation_id=None) -> bytes:
         try:
-            positions_json = json.loads(body.decode())
-            positions = [Point(x) for x in positions_json["positions"]]
-            angles_dict = dict()
-            angles = self.ikine.ikine(positions)
-        except (OutOfRobotReachException, ValueError, TypeError) as exception:
-            debug_msg_print(str(exception))
-            angles_dict = exception_response("ERROR", str(exception), correlation_id)
-        else:
-            angles_dict["status"] = "OK"
-            angles_dict["angles"] = angles
-        return json.dumps(angles_dict).encode()
+            reply = ok_reply(self.ikine.ikine(decode_request(body)))
+        except REPLY_ERRORS as exc:
+            log.debug("request %s refused: %s", correlation_id, exc)
+            reply = error_reply(exc, correlation_id)
+        return json.dumps(reply).encode()
+
+
+def build_engine(method: str, model: Optional[str] = None):
+    """The SixDOFRobot engine of `method` (with `model` loaded for ann)."""
+    if method == "ann":
+        engine = AnnInverseKinematics(Robot.dh_matrix, Robot.links_lengths,
+                                      Robot.effector_workspace_limits)
+        engine.load_model(model)
+        return engine
+    return FabrikInverseKinematics(Robot.dh_matrix, Robot.links_lengths,
+                                   Robot.effector_workspace_limits)
+
+
+def get_ikine_engine_cli(argv: Optional[Sequence[str]] = None):
+    """The engine named on the command line: --method {ann,fabrik} [--model M.h5]."""
+    parser = argparse.ArgumentParser(prog="rpc_broker",
+                                     description="serve IK requests from a RabbitMQ queue")
+    parser.add_argument("--method", required=True, choices=["ann", "fabrik"],
+                        help="IK engine behind the queue")
+    parser.add_argument("--model", help="Keras .h5 model (with its _scaler_x/_y.bin files); "
+                                        "needed by --method ann")
+    args = parser.parse_args(argv)
+    if args.method == "ann" and not args.model:
+        parser.error("--method ann needs --model")
+    return build_engine(args.method, args.model)
 
 
 class IkineRPCBroker:
-    """rpc_broker.py:57-104 on the GPU engine (requires the pika client)."""
+    """RabbitMQ consumer of RPC_QUEUE: each request is answered on its reply_to
+    queue with the same correlation id, then acknowledged (prefetch 1)."""
 
-    def __init__(self, ikine, host_ip="rabbit_mq", queue_name="ikine_queue"):
+    def __init__(self, ikine, host_ip: str = RPC_HOST, queue_name: str = RPC_QUEUE):
         try:
-            from pika import BasicProperties, BlockingConnection, ConnectionParameters
-        except ImportError as e:  # transport is optional; the handler is not
+            import pika
+        except ImportError as e:  # the transport is optional, the handler is not
             raise RuntimeError("IkineRPCBroker needs the 'pika' RabbitMQ client, which is not "
                                "installed; IkineRequestHandler serves the same payloads") from e
-        self._props = BasicProperties
-        self._handler = IkineRequestHandler(ikine)
-        self._connection = BlockingConnection(ConnectionParameters(host=host_ip))
-        self._channel = self._connection.channel()
-        self._channel.queue_declare(queue=queue_name)
-        self._channel.basic_qos(prefetch_count=1)
-        self._channel.basic_consume(queue=queue_name, on_message_callback=self.callback)
+        self._pika = pika
+        self.handler = IkineRequestHandler(ikine)
+        self.connection = pika.BlockingConnection(pika.ConnectionParameters(host=host_ip))
+        self.channel = self.connection.channel()
+        self.channel.queue_declare(queue=queue_name)
+        self.channel.basic_qos(prefetch_count=1)
+        self.channel.basic_consume(queue=queue_name, on_message_callback=self._on_request)
 
-    def callback(self, chan, method, props, body):
-        resp = self._handler.handle(body, props.correlation_id)
-        chan.basic_publish(exchange="", routing_key=props.reply_to,
-                           properties=self._props(correlation_id=props.correlation_id),
-                           body=resp)
-        chan.basic_ack(delivery_tag=method.delivery_tag)
+    def _on_request(self, channel, delivery, props, body):
+        reply = self.handler.handle(body, props.correlation_id)
+        channel.basic_publish(exchange="", routing_key=props.reply_to, body=reply,
+                              properties=self._pika.BasicProperties(
+                                  correlation_id=props.correlation_id))
+        channel.basic_ack(delivery_tag=delivery.delivery_tag)
 
-    def start(self):
-        self._channel.start_consuming()
+    def serve(self):
+        self.channel.start_consuming()
 
+    start = serve
 
-def main(argv=None):
-    try:
-        broker = IkineRPCBroker(get_ikine_engine_cli(argv))
-        broker.start()
-    except KeyboardInterrupt:
-        print("CTRL+C interrupted")
+    def close(self):
         try:
-            sys.exit(0)
-        except SystemExit:
-            os._exit(0)
+            self.channel.stop_consuming()
+        finally:
+            self.connection.close()
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    broker = IkineRPCBroker(get_ikine_engine_cli(argv))
+    try:
+        broker.serve()
+    except KeyboardInterrupt:
+        log.info("interrupted; closing the connection")
+        broker.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main())

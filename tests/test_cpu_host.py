@@ -96,3 +96,44 @@ def test_point_helpers():
     assert [-2.22, 3.123, 0.002] == p1
     np.testing.assert_almost_equal(3.831649, get_distance_between(p0, p1))
     np.testing.assert_almost_equal((np.array(p0) + np.array(p1)) / 2, get_point_between(p0, p1))
+
+
+def test_points_of_the_wrong_width_raise(tmp_path, capsys):
+    """A 4-column CSV (e.g. written with pandas index=True) is not reinterpreted as
+    other points: FABRIK raises the reference Point's ValueError (point.py:12-14),
+    ANN the StandardScaler's feature-count error, and the CLI prints it and exits 0
+    (cli.py:250-252).  Host-side checks: nothing reaches the GPU."""
+    import pandas as pd
+    from inversekinematicsann_amd.cli import main
+    from inversekinematicsann_amd.kinematics.ann import as_features
+    from inversekinematicsann_amd.kinematics.inverse import as_points
+    with pytest.raises(ValueError, match=r"3D Point input shape should be \(3,\) not \(4,\)"):
+        as_points(np.ones((3, 4)))
+    with pytest.raises(ValueError, match=r"not \(2,\)"):
+        as_points([[1.0, 2.0], [3.0, 4.0]])
+    with pytest.raises(ValueError, match="X has 4 features, but StandardScaler is expecting 3"):
+        as_features(np.ones((3, 4)))
+    assert as_points([]).shape == (0, 3) and as_features([1.0, 2.0, 3.0]).shape == (1, 3)
+    csv = tmp_path / "pts4.csv"
+    pd.DataFrame([[1.0, 2.0, 3.0], [1.5, 2.5, 3.5], [1.0, 1.0, 1.0]],
+                 columns=["x", "y", "z"]).to_csv(csv, index=True)
+    rc = main(["--inverse-kine", "--method", "fabrik", "--points", str(csv)])
+    assert rc == 0
+    assert capsys.readouterr().out.strip() == "3D Point input shape should be (3,) not (4,)"
+
+
+def test_scaler_flags_reach_the_kernel_constants():
+    """with_mean / with_std off: the kernels get mean 0 / scale 1, so the fused
+    (x - mean) / scale and y * scale + mean equal sklearn's skipped steps."""
+    from inversekinematicsann_amd.models.scaler_bin import ScalerParams
+    sp = ScalerParams(mean=np.array([1.0, 2.0, 3.0]), scale=np.array([2.0, 4.0, 8.0]), var=None,
+                      with_mean=False, with_std=True)
+    m, s = sp.effective()
+    assert m.tolist() == [0.0, 0.0, 0.0] and s.tolist() == [2.0, 4.0, 8.0]
+    x = np.array([[1.0, 2.0, 3.0]])
+    assert np.array_equal((x - m) / s, sp.transform(x))
+    sp = ScalerParams(mean=np.array([1.0, 2.0, 3.0]), scale=np.array([2.0, 4.0, 8.0]), var=None,
+                      with_mean=True, with_std=False)
+    m, s = sp.effective()
+    assert m.tolist() == [1.0, 2.0, 3.0] and s.tolist() == [1.0, 1.0, 1.0]
+    assert np.array_equal((x - m) / s, sp.transform(x))

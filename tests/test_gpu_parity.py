@@ -459,3 +459,58 @@ def test_fk_full_angle_range_vs_oracle():
     ok[[37, 60]] = False
     assert np.abs(xyz[ok] - rxyz[ok]).max() <= 1e-12
     c.close()
+
+
+def test_robot_state_per_object_interleaved():
+    """Objects with different robots interleave on the one process context:
+    FABRIK with custom links, then fkine of another object, then FABRIK again --
+    every result equals the oracle for its own robot, and fkine leaves the links
+    and limits alone (it uploads only its DH table)."""
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.kinematics.forward import ForwardKinematics
+    from inversekinematicsann_amd.kinematics.inverse import FabrikInverseKinematics
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    from inversekinematicsann_amd.robot.robot import SixDOFRobot
+    robot = SixDOFRobot()
+    dh = [list(r) for r in robot.dh_matrix]
+    links = [2.0, 2.0, 2.5, 2.5]
+    lim = robot.effector_workspace_limits
+    pts = random_dist(2000, seed=31)
+    ik_a = FabrikInverseKinematics([list(r) for r in dh], links, lim)
+    ik_b = FabrikInverseKinematics([list(r) for r in dh], robot.links_lengths, lim)
+    ra, rit_a, _, _ = O.fabrik_ikine(pts, 1e-3, 100, links=np.array(links))
+    rb, rit_b, _, _ = O.fabrik_ikine(pts, 1e-3, 100)
+    a1 = np.array(ik_a.ikine(pts))
+    m4, _ = ForwardKinematics([list(r) for r in dh]).fkine([0.1, 0.2, 0.3, 0.4])
+    rxyz, _, _ = O.fk(np.array([[0.1, 0.2, 0.3, 0.4]]))
+    assert np.abs(m4[:3, 3] - rxyz[0]).max() <= 1e-12
+    a2 = np.array(ik_a.ikine(pts))  # the links must still be ik_a's
+    b1 = np.array(ik_b.ikine(pts))
+    a3 = np.array(ik_a.ikine(pts))
+    for got, ref in ((a1, ra), (a2, ra), (b1, rb), (a3, ra)):
+        assert np.abs(got - ref).max() <= 1e-9
+    assert np.array_equal(ik_a.last_iterations, rit_a)
+    assert np.array_equal(ik_b.last_iterations, rit_b)
+    ctx = _native.context()
+    n0 = ctx.robot_uploads
+    ik_a.ikine(pts)
+    ik_a.ikine(pts)  # same robot, only dh[0][0] changed by the quirk: no upload
+    assert ctx.robot_uploads == n0 + 1  # ik_b's robot -> ik_a's, once
+
+
+def test_cli_call_uploads_the_robot_at_most_once():
+    """A 20-point CLI call (cli.py --inverse-kine --method fabrik) makes at most one
+    ik_set_robot in the process (none when the context already holds the robot)."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.argv=['ik_cli','--inverse-kine','--method','fabrik','--points',"
+            f"{os.path.join(GOLDEN, 'cli_spring20_points.csv')!r},'--verbose'];"
+            "from inversekinematicsann_amd.cli import main; rc=main(sys.argv[1:]);"
+            "from inversekinematicsann_amd import _native;"
+            "print('UPLOADS', _native.context().robot_uploads)")
+    from tests.conftest import ROOT
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=120, cwd=ROOT)
+    line = [l for l in out.stdout.splitlines() if l.startswith("UPLOADS")]
+    assert line, out.stdout + out.stderr
+    assert int(line[0].split()[1]) <= 1
