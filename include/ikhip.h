@@ -123,7 +123,8 @@ int ik_fabrik_calc(ik_ctx *ctx, int nj, const double *dists, const double *init,
  * Dense layers, dims[0..n_layers] (dims[0] == 3, dims[n_layers] == 4), acts[l]
  * one of IK_ACT_*, W[l] host float32 [dims[l]][dims[l+1]] row-major (the Keras
  * kernel layout, x @ W + b), b[l] host float32 [dims[l+1]], and the two
- * StandardScalers (ann.py:83-84).  Widths up to 512. */
+ * StandardScalers (ann.py:83-84).  Widths up to 1024 (models wider than 512 run
+ * the fp32 kernel whatever ik_ann_set_mode says). */
 int ik_ann_load(ik_ctx *ctx, int n_layers, const int32_t *dims, const int32_t *acts,
                 const float *const *W, const float *const *b, const double *x_mean,
                 const double *x_scale, const double *y_mean, const double *y_scale);

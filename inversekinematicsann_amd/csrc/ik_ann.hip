@@ -16,9 +16,10 @@
 // pre-packed "MFMA fragment" order (one 1 KiB dwordx4 load per 8-deep K group
 // and column tile), triple-buffered two K groups ahead.  Bias + activation are
 // applied on the accumulators and written back over the tile in LDS.
-//   MR = 2: 64-point tiles, 129 KiB LDS, one workgroup per CU (max weight reuse);
+//   MR = 2: 64-point tiles, 129 KiB LDS, one workgroup per CU (max weight reuse;
+//           the split modes' default);
 //   MR = 1: 32-point tiles, 64.5 KiB LDS, two workgroups per CU, so one
-//           workgroup's barrier / epilogue overlaps the other's MFMAs.
+//           workgroup's barrier / epilogue overlaps the other's MFMAs (fp32 default).
 // The grid is persistent: workgroups walk the point tiles.
 #include <cmath>
 #include <cstring>
@@ -26,11 +27,26 @@
 #include "ik_common.h"
 
 namespace ikhip {
+// The device code is compiled twice: for widths <= 512 (this TU and ik_ann_x.hip,
+// namespace ann) and for widths <= 1024 (ik_ann_w.hip, IKHIP_ANN_WIDE, namespace
+// annw: 1028-float rows, 32-point tiles, up to 8 column tiles per wave).  The
+// inline device functions of the two builds differ (kLd), hence the namespaces.
+#ifdef IKHIP_ANN_WIDE
+namespace annw {
+#else
+namespace ann {
+#endif
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+#ifdef IKHIP_ANN_WIDE
+constexpr int kLd = 1028;  // LDS row stride in floats (>= 1024 + 4)
+constexpr bool kWide = true;
+#else
 constexpr int kLd = 516;   // LDS row stride in floats (>= 512 + 4)
+constexpr bool kWide = false;
+#endif
 constexpr int kWaves = 4;  // waves per workgroup
 constexpr int kHPad = 64;  // floats past the last activation row (see layer_gemm)
 
@@ -704,7 +720,7 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 // (a.m.wx[l]) take the split GEMM; the others (input layer, split-K output
 // layer, fp16x3-ineligible layers) stay fp32.
 template <int MR, int X>
-__global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnArgs a) {
+__global__ __launch_bounds__(256, (MR == 2 || kWide) ? 1 : 2) void ann_fused_kernel(AnnArgs a) {
   constexpr int BM = 32 * MR;
   // + kHPad: the fp32 GEMM's operand ring reads up to 3 K groups past a row's end
   __shared__ __attribute__((aligned(16))) float H[BM * kLd + kHPad];
@@ -772,6 +788,12 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
           case 3: run_layer<MR, 3>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
           case 2: run_layer<MR, 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
           case 1: run_layer<MR, 1>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+#ifdef IKHIP_ANN_WIDE
+          case 8: run_layer<MR, 8>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 7: run_layer<MR, 7>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 6: run_layer<MR, 6>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 5: run_layer<MR, 5>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+#endif
           default: __syncthreads(); break;  // idle wave still joins the barrier
         }
       }
@@ -819,7 +841,42 @@ __global__ __launch_bounds__(256, (MR == 2) ? 1 : 2) void ann_fused_kernel(AnnAr
 // spilled VGPRs at MR = 2, -Rpass-analysis=kernel-resource-usage).
 void launch_ann_kernel_x(int mr, int xmode, unsigned grid, hipStream_t st, const AnnArgs &a);
 
-#ifndef IKHIP_ANN_X_TU
+}  // namespace ann / annw
+
+#if defined(IKHIP_ANN_WIDE)
+
+// Models wider than 512 (up to 1024): fp32 only, 32-point tiles (132 KiB of
+// LDS: one workgroup per CU).
+void launch_ann_wide(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
+                     float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
+                     unsigned long long *dbg) {
+  using namespace annw;
+  if (n <= 0) return;
+  AnnArgs a;
+  a.m = m;
+  a.r = r;
+  a.pts = pts;
+  a.n = n;
+  a.ang = ang;
+  a.fk_err = fk_err;
+  a.check_limits = check_limits ? 1 : 0;
+  a.S = S;
+  a.dbg = dbg;
+  fk_trip_consts(r, a.jc, &a.alpha_bad);
+  int dev = 0, cus = 256;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  const int64_t ntiles = (n + 31) / 32;
+  const unsigned grid = (unsigned)(ntiles < cus ? ntiles : cus);
+  kt_begin("ann_fused_kernel_wide", st);
+  hipLaunchKernelGGL((ann_fused_kernel<1, 0>), dim3(grid), dim3(256), 0, st, a);
+  kt_end(st);
+}
+
+#elif !defined(IKHIP_ANN_X_TU)
+using namespace ann;
 
 size_t ann_packed_floats(int k, int n) {
   int kp = (k + 7) / 8 * 8, np = (n + 31) / 32 * 32;
@@ -936,16 +993,20 @@ void ann_pack_layer_h(const float *W, int k, int n, int scale_exp, void *dst) {
         }
 }
 
-static int ann_tile_rows() {
-  static int mr = 0;
-  if (mr == 0) {
-    // MR = 2 measured faster on MI355X (1M points, 3-12x500-4): 44.9 ms vs 49.0 ms
-    // (tools/sweep_ann.py): the halved weight reuse of MR = 1 costs more than
-    // the epilogue overlap it buys.
+// Tile rows per workgroup: 32 * MR points.  fp32: MR = 1 (two 32-point
+// workgroups per CU, one's barrier and epilogue under the other's MFMAs)
+// measured 39.8 ms against 41.3 ms for MR = 2 (1M points, 3-12x500-4,
+// tools/sweep_ann.py and bench.py, same box; round 1's GEMM loop measured the
+// opposite, 49.0 vs 44.9 ms).  The split modes keep MR = 2: their GEMM is bound
+// by the weight stream from L2, which 64-point tiles halve (bf16x6 25.1 vs
+// 33.8 ms, fp16x3 15.2 vs 19.6 ms).  IKHIP_ANN_MR overrides.
+static int ann_tile_rows(int xmode) {
+  static int forced = -1;
+  if (forced < 0) {
     const char *v = getenv("IKHIP_ANN_MR");
-    mr = (v && atoi(v) == 1) ? 1 : 2;
+    forced = (v && (atoi(v) == 1 || atoi(v) == 2)) ? atoi(v) : 0;
   }
-  return mr;
+  return forced ? forced : (xmode ? 2 : 1);
 }
 
 size_t ann_debug_words() { return (size_t)kStampTiles * kWaves * kStampSlots; }
@@ -954,6 +1015,11 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
                 float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
                 unsigned long long *dbg) {
   if (n <= 0) return;
+  for (int l = 0; l < m.n_layers; ++l)
+    if (m.np[l] > 512 || m.kp[l] > 512) {
+      launch_ann_wide(m, r, pts, n, ang, fk_err, check_limits, S, st, dbg);
+      return;
+    }
   AnnArgs a;
   a.m = m;
   a.r = r;
@@ -970,14 +1036,14 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
       cus <= 0)
     cus = 256;
-  const int mr = ann_tile_rows();
+  bool x = false;
+  for (int l = 0; l < m.n_layers; ++l) x = x || m.wx[l] != nullptr;
+  const int xmode = x ? m.xmode : 0;
+  const int mr = ann_tile_rows(xmode);
   const int64_t bm = 32 * mr;
   const int64_t ntiles = (n + bm - 1) / bm;
   const int64_t slots = (int64_t)cus * (mr == 2 ? 1 : 2);  // resident workgroups
   unsigned grid = (unsigned)(ntiles < slots ? ntiles : slots);
-  bool x = false;
-  for (int l = 0; l < m.n_layers; ++l) x = x || m.wx[l] != nullptr;
-  const int xmode = x ? m.xmode : 0;
   kt_begin(xmode == 1 ? "ann_fused_kernel_bf16x6"
                       : xmode == 2 ? "ann_fused_kernel_fp16x3" : "ann_fused_kernel",
            st);
@@ -992,7 +1058,8 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
 
 #else  // IKHIP_ANN_X_TU
 
-void launch_ann_kernel_x(int mr, int xmode, unsigned grid, hipStream_t st, const AnnArgs &a) {
+void ann::launch_ann_kernel_x(int mr, int xmode, unsigned grid, hipStream_t st,
+                              const AnnArgs &a) {
 #define IK_X(M, X) hipLaunchKernelGGL((ann_fused_kernel<M, X>), dim3(grid), dim3(256), 0, st, a)
   if (mr == 2) {
     if (xmode == 2) IK_X(2, 2); else IK_X(2, 1);

@@ -503,7 +503,10 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   // single-column-tile output layer) -- the split bf16 planes
   std::vector<size_t> woff(n_layers), boff(n_layers), xoff(n_layers, 0), hoff(n_layers, 0);
   std::vector<int> hexp(n_layers, 0);
-  auto splittable = [&](int l) { return l > 0 && (dims[l + 1] + 31) / 32 > 1; };
+  // models wider than 512 run the wide fp32 kernel only: no split operands
+  bool wide = false;
+  for (int l = 0; l <= n_layers; ++l) wide = wide || dims[l] > 512;
+  auto splittable = [&](int l) { return !wide && l > 0 && (dims[l + 1] + 31) / 32 > 1; };
   // fp16x3 also needs a bounded layer input: the layer before is tanh or sigmoid
   auto halvable = [&](int l) {
     return splittable(l) && (acts[l - 1] == IK_ACT_TANH || acts[l - 1] == IK_ACT_SIGMOID);

@@ -515,7 +515,7 @@ void launch_fabrik_calc(int nj, const double *dists, const double *init, bool in
                         double *joints, int32_t *iters, DevStats *S, hipStream_t st);
 
 constexpr int kAnnMaxLayers = 24;
-constexpr int kAnnMaxWidth = 512;
+constexpr int kAnnMaxWidth = 1024;  // > 512: the wide build (ik_ann_w.hip), fp32 only
 struct AnnModelDev {
   int n_layers;
   int kp[kAnnMaxLayers];  // padded in-dim (multiple of 8)
@@ -539,4 +539,7 @@ size_t ann_debug_words();  // u64 slots of the diagnostic stamp buffer
 void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
                 float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
                 unsigned long long *dbg);
+void launch_ann_wide(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
+                     float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
+                     unsigned long long *dbg);
 }  // namespace ikhip

@@ -239,6 +239,10 @@ def _ann_case(ctx, dims, acts_hidden, n, seed, check_limits=False, fk=False):
     # full-width layers whose K is padded to 64 past what the layer before wrote
     ((3, 450, 500, 4), "tanh"),
     ((3, 70, 512, 4), "sigmoid"),
+    # wider than 512: the wide build (1028-float LDS rows, 32-point tiles)
+    ((3, 1024, 1024, 4), "tanh"),
+    ((3, 768, 500, 4), "tanh"),
+    ((3, 600, 1000, 37, 4), "relu"),
 ])
 def test_ann_vs_oracle(ctx1, dims, act):
     n = 4099  # not a multiple of the 64-point tile
@@ -246,6 +250,18 @@ def test_ann_vs_oracle(ctx1, dims, act):
     assert ang.dtype == np.float32 and ang.shape == (n, 4)
     d = np.abs(ang.astype(np.float64) - ref64).max()
     assert d <= NS_TOL, d  # north_star: 1e-5 absolute
+
+
+def test_ann_width_cap(ctx1):
+    """ik_ann_load takes widths up to 1024 and refuses only wider layers."""
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER as XS, \
+        REFERENCE_Y_SCALER as YS
+    m = glorot_model(dims=(3, 1025, 4), seed=1)
+    with pytest.raises(_native.NativeError, match="1..1024"):
+        ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    m = glorot_model(dims=(3, 1024, 4), seed=1)
+    ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
 
 
 @pytest.mark.parametrize("mode", ["bf16x6", "fp16x3"])
@@ -494,8 +510,10 @@ def test_robot_state_per_object_interleaved():
     ctx = _native.context()
     n0 = ctx.robot_uploads
     ik_a.ikine(pts)
-    ik_a.ikine(pts)  # same robot, only dh[0][0] changed by the quirk: no upload
-    assert ctx.robot_uploads == n0 + 1  # ik_b's robot -> ik_a's, once
+    ik_a.ikine(pts)  # the context holds ik_a's robot (dh[0][0] moves, unread): no upload
+    assert ctx.robot_uploads == n0
+    ik_b.ikine(pts)
+    assert ctx.robot_uploads == n0 + 1
 
 
 def test_cli_call_uploads_the_robot_at_most_once():
@@ -514,3 +532,37 @@ def test_cli_call_uploads_the_robot_at_most_once():
     line = [l for l in out.stdout.splitlines() if l.startswith("UPLOADS")]
     assert line, out.stdout + out.stderr
     assert int(line[0].split()[1]) <= 1
+
+
+def test_ann_tile_variants_agree(ctx1, tmp_path):
+    """fp32 runs 32-point tiles by default (MR = 1), the split modes 64 (MR = 2);
+    IKHIP_ANN_MR forces either.  The other tile size, in a fresh process, gives
+    the same bits (per point the same K order and the same fixed split-K sum)."""
+    import subprocess
+    import sys
+    from tests.conftest import ROOT
+    from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER as XS, \
+        REFERENCE_Y_SCALER as YS
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    dims = (3, 200, 300, 4)
+    m = glorot_model(dims=dims, seed=9)
+    pts = random_dist(5000, seed=9)
+    ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    mine, err, _ = ctx1.ann_solve(pts, want_fk_err=True)
+    out = tmp_path / "mr2.npz"
+    code = (
+        "import numpy as np\n"
+        "from inversekinematicsann_amd import _native\n"
+        "from inversekinematicsann_amd.kinematics.ann import glorot_model, "
+        "REFERENCE_X_SCALER as XS, REFERENCE_Y_SCALER as YS\n"
+        "from inversekinematicsann_amd.robot.position_generator import random_dist\n"
+        f"m = glorot_model(dims={dims!r}, seed=9); pts = random_dist(5000, seed=9)\n"
+        "c = _native.Context(0)\n"
+        "c.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)\n"
+        "a, e, _ = c.ann_solve(pts, want_fk_err=True)\n"
+        f"np.savez({str(out)!r}, a=a, e=e)\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120, env=dict(os.environ, IKHIP_ANN_MR="2"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    other = np.load(out)
+    assert np.array_equal(mine, other["a"]) and np.array_equal(err, other["e"])
