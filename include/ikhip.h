@@ -92,6 +92,14 @@ int ik_check_limits(ik_ctx *ctx, const double *pts, int64_t n, int flags, ik_sta
 int ik_fk(ik_ctx *ctx, const double *ang, int64_t n, double *xyz, double *mats, int flags,
           ik_stats *stats);
 
+/* ForwardKinematics(dh).fkine for a DH table of nj (2..8) joints (the reference
+ * takes any nj >= 3, forward.py:13-19): dh host 4 x nj row-major (thetas, d, a,
+ * alpha), ang n x nj -> effector xyz n x 3 and, if mats is not NULL, the nj
+ * cumulative 4 x 4 transforms (n x nj x 16; the reference's nj x nj matrices
+ * are these embedded in the identity). */
+int ik_fk_chain(ik_ctx *ctx, int nj, const double *dh, const double *ang, int64_t n, double *xyz,
+                double *mats, int flags, ik_stats *stats);
+
 /* ---- FABRIK ---------------------------------------------------------------
  * FabrikInverseKinematics.ikine, kinematics/inverse.py:115-139 (+ check_limits,
  * Fabrik.calculate fabrik.py:44-67, __get_angles inverse.py:54-112), batched:

@@ -29,7 +29,7 @@ IK_F_DEVICE, IK_F_ASYNC, IK_F_NO_LIMITS = 1, 2, 4
 ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
 
 EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_ctx_get_stream",
-                    "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk",
+                    "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk", "ik_fk_chain",
                     "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode",
@@ -110,6 +110,7 @@ def load_library(path: str = LIB_PATH):
         L.ik_set_robot.argtypes = [vp, dp, dp, dp]
         L.ik_check_limits.argtypes = [vp, dp, i64, ctypes.c_int, st]
         L.ik_fk.argtypes = [vp, dp, i64, dp, dp, ctypes.c_int, st]
+        L.ik_fk_chain.argtypes = [vp, ctypes.c_int, dp, dp, i64, dp, dp, ctypes.c_int, st]
         L.ik_fabrik_solve.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp, ctypes.c_int,
                                       st]
         L.ik_fabrik_solve_fk.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp, dp,
@@ -235,6 +236,22 @@ class Context:
         mats = np.empty((n, 4, 4, 4), np.float64) if with_mats else None
         self._check(self.lib.ik_fk(self.handle, _ptr(a), n, _ptr(xyz), _ptr(mats), 0,
                                    ctypes.byref(s)))
+        return xyz, mats, s
+
+    def fk_chain(self, dh, ang, with_mats: bool = False):
+        """FK of an nj-joint DH table (4 x nj): returns (xyz n x 3, mats n x nj x 4 x 4
+        or None, stats)."""
+        d = _host(dh, np.float64)
+        if d.ndim != 2 or d.shape[0] != 4:
+            raise ValueError("dh must be 4 x nj")
+        nj = d.shape[1]
+        a = _host(ang, np.float64, nj)
+        n = a.shape[0]
+        xyz = np.empty((n, 3), np.float64)
+        mats = np.empty((n, nj, 4, 4), np.float64) if with_mats else None
+        s = IkStats()
+        self._check(self.lib.ik_fk_chain(self.handle, nj, _ptr(d), _ptr(a), n, _ptr(xyz),
+                                         _ptr(mats), 0, ctypes.byref(s)))
         return xyz, mats, s
 
     def fk_device(self, ang, xyz, flags: int = IK_F_DEVICE):

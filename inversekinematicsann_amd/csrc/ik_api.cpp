@@ -371,6 +371,47 @@ int ik_fk(ik_ctx *c, const double *ang, int64_t n, double *xyz, double *mats, in
   return finish(c, flags, stats);
 }
 
+int ik_fk_chain(ik_ctx *c, int nj, const double *dh, const double *ang, int64_t n,
+                double *xyz, double *mats, int flags, ik_stats *stats) {
+  if (!c || nj < 2 || nj > 8 || !dh || n < 0 || (n > 0 && (!ang || !xyz)))
+    return fail(IK_E_BADARG, "ik_fk_chain: bad args (nj must be 2..8)");
+  if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
+    return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);
+  const bool dev = flags & IK_F_DEVICE;
+  const size_t b_dh = Stage::up((size_t)nj * 32);
+  const size_t b_in = dev ? 0 : Stage::up((size_t)n * nj * 8);
+  const size_t b_x = dev ? 0 : Stage::up((size_t)n * 24);
+  const size_t b_m = (dev || !mats) ? 0 : Stage::up((size_t)n * nj * 128);
+  if ((rc = ensure_scratch(c, b_dh + b_in + b_x + b_m))) return rc;
+  char *s = static_cast<char *>(c->scratch);
+  // the DH table always travels from host memory
+  IK_HIP(hipMemcpyAsync(s, dh, (size_t)nj * 32, hipMemcpyHostToDevice, c->stream));
+  const double *dd = reinterpret_cast<const double *>(s);
+  const double *da = ang;
+  double *dx = xyz, *dm = mats;
+  if (!dev) {
+    char *q = s + b_dh;
+    IK_HIP(hipMemcpyAsync(q, ang, (size_t)n * nj * 8, hipMemcpyHostToDevice, c->stream));
+    da = reinterpret_cast<const double *>(q);
+    dx = reinterpret_cast<double *>(q + b_in);
+    dm = mats ? reinterpret_cast<double *>(q + b_in + b_x) : nullptr;
+  }
+  launch_reset_stats(c->d_stats, c->stream);
+  launch_fk_n(nj, dd, da, n, dx, dm, c->d_stats, c->stream);
+  IK_HIP(hipGetLastError());
+  if (!dev && n > 0) {
+    IK_HIP(hipMemcpyAsync(xyz, dx, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    if (mats)
+      IK_HIP(hipMemcpyAsync(mats, dm, (size_t)n * nj * 128, hipMemcpyDeviceToHost, c->stream));
+  }
+  // dh came from a host buffer that may go away: always complete before return
+  if (flags & IK_F_ASYNC) IK_HIP(hipStreamSynchronize(c->stream));
+  return finish(c, flags, stats);
+}
+
 int ik_fabrik_solve(ik_ctx *c, const double *pts, int64_t n, double tol, int32_t max_iter,
                     double *ang, int32_t *iters, double *joints, int flags, ik_stats *stats) {
   return ik_fabrik_solve_fk(c, pts, n, tol, max_iter, ang, iters, joints, nullptr, flags, stats);

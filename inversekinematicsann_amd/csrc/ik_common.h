@@ -485,6 +485,9 @@ void launch_check_limits(const RobotDev &r, const double *pts, int64_t n, DevSta
                          hipStream_t st);
 void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, double *mats,
                DevStats *S, hipStream_t st);
+// FK of a chain of nj (2..8) joints; dh: device 4 x nj, mats nullable n x nj x 16.
+void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double *xyz,
+                 double *mats, DevStats *S, hipStream_t st);
 // FABRIK work order (ik_fabrik.hip "Work order"): per context, the largest
 // iteration count recorded in each goal cell (distance x elevation from the
 // shoulder) on the context's earlier calls decides which points start first.

@@ -162,6 +162,69 @@ __global__ __launch_bounds__(256) void fk_kernel(RobotDev r, FkConst kc,
   }
 }
 
+// ForwardKinematics.fkine for a chain of NJ joints (forward.py:11-94 accepts any
+// number of features >= 3; 4 is the robot's own): dh is 4 x NJ row-major (thetas,
+// d, a, alpha), ang n x NJ.  The reference builds NJ x NJ matrices whose
+// upper-left 4 x 4 block is the usual DH transform and whose remaining rows and
+// columns are the identity, so every product is that block's product: the
+// kernel forms the 4 x 4 chain (dh_transform + mm4, the same as fk_chain) and
+// the host embeds it.  Angles are checked joint by joint, theta then alpha
+// (forward.py:23-25 raises on the first).
+template <int NJ>
+__global__ __launch_bounds__(256) void fk_n_kernel(const double *__restrict__ dh,
+                                                    const double *__restrict__ ang, int64_t n,
+                                                    double *__restrict__ xyz,
+                                                    double *__restrict__ mats, DevStats *S) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int st = IK_OK;
+  double M[16], A[16];
+#pragma unroll
+  for (int k = 0; k < NJ; ++k) {
+    const double th = ang[(size_t)i * NJ + k];
+    if (!angle_ok(th) || !angle_ok(dh[3 * NJ + k])) st = IK_E_ANGLE_RANGE;
+    dh_transform(th, dh[NJ + k], dh[2 * NJ + k], dh[3 * NJ + k], k == 0 ? M : A);
+    if (k > 0) mm4(M, A, M);
+    if (mats) {
+      double *o = mats + ((size_t)i * NJ + k) * 16;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[e] = M[e];
+    }
+  }
+  d3 e = {M[3], M[7], M[11]};
+  if (st != IK_OK) {
+    record_error(S, i, st);
+    e.x = e.y = e.z = __builtin_nan("");
+  }
+  xyz[3 * i] = e.x;
+  xyz[3 * i + 1] = e.y;
+  xyz[3 * i + 2] = e.z;
+}
+
+void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double *xyz,
+                 double *mats, DevStats *S, hipStream_t st) {
+  if (n <= 0) return;
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  kt_begin("fk_n_kernel", st);
+#define IK_FKN(K)                                                                           \
+  case K:                                                                                   \
+    hipLaunchKernelGGL(fk_n_kernel<K>, dim3(grid), dim3(256), 0, st, dh, ang, n, xyz, mats, S); \
+    break;
+  switch (nj) {
+    IK_FKN(2)
+    IK_FKN(3)
+    IK_FKN(4)
+    IK_FKN(5)
+    IK_FKN(6)
+    IK_FKN(7)
+    IK_FKN(8)
+    default:
+      break;
+  }
+#undef IK_FKN
+  kt_end(st);
+}
+
 static int fk_cus() {
   int dev = 0, cus = 0;
   (void)hipGetDevice(&dev);

@@ -7,6 +7,8 @@ per lane, float64 DH chain).  fkine_batch(angles) is the batched entry point
 """
 from __future__ import annotations
 
+from math import pi
+
 import numpy as np
 
 from .. import _native
@@ -24,8 +26,8 @@ class ForwardKinematics:
         self.thetas, self.epsilons, self.ais, self.alphas = self.dh_matrix
         self.no_of_features = len(self.thetas)
         assert self.no_of_features >= 3
-        if self.no_of_features != 4:
-            raise NotImplementedError('the HIP FK kernel implements 4-joint DH chains')
+        if self.no_of_features > 8:
+            raise NotImplementedError('the HIP FK kernels take DH chains of 3 to 8 joints')
 
     def _ctx(self):
         """The process context with this object's DH table; the link lengths and
@@ -34,18 +36,46 @@ class ForwardKinematics:
         ctx.set_robot(np.asarray(self.dh_matrix, np.float64))
         return ctx
 
+    def _three_features(self, angles):
+        # forward.py with 3 features: __rotation_matrix checks the angle, then
+        # returns the axis name (its matrix is already 3 x 3, :42-43), and
+        # __translation_matrix writes column 3 of a 3 x 3 identity (:56-59)
+        if angles[0] < -2 * pi or angles[0] > 2 * pi:
+            raise OutOfRobotReachException(_ANGLE_MSG)
+        raise IndexError('index 3 is out of bounds for axis 1 with size 3')
+
     def fkine(self, angles):
-        """(end transform, [all four cumulative transforms]) for one angle vector."""
+        """(end transform, [all cumulative transforms]) for one angle vector:
+        no_of_features x no_of_features matrices, as the reference builds them."""
         self.thetas = angles
-        _, mats, st = self._ctx().fk(np.asarray([angles], np.float64), with_mats=True)
+        nf = self.no_of_features
+        if nf == 3:
+            self._three_features(angles)
+        if nf == 4:
+            _, mats, st = self._ctx().fk(np.asarray([angles], np.float64), with_mats=True)
+        else:
+            _, mats, st = _native.context().fk_chain(np.asarray(self.dh_matrix, np.float64),
+                                                     np.asarray([angles], np.float64),
+                                                     with_mats=True)
         if st.first_err >= 0:
             raise OutOfRobotReachException(_ANGLE_MSG)
-        ms = [mats[0, k].copy() for k in range(4)]
+        ms = []
+        for k in range(nf):
+            m = np.identity(nf)
+            m[:4, :4] = mats[0, k]  # the 4 x 4 DH block; the rest is the identity
+            ms.append(m)
         return ms[-1], ms
 
     def fkine_batch(self, angles) -> np.ndarray:
         """Effector positions (n x 3 float64) of n angle vectors."""
-        xyz, _, st = self._ctx().fk(angles)
+        nf = self.no_of_features
+        if nf == 4:
+            xyz, _, st = self._ctx().fk(angles)
+        else:
+            a = np.asarray(angles, np.float64).reshape(-1, nf)
+            if nf == 3 and len(a):
+                self._three_features(a[0])
+            xyz, _, st = _native.context().fk_chain(np.asarray(self.dh_matrix, np.float64), a)
         if st.first_err >= 0:
             raise OutOfRobotReachException(_ANGLE_MSG)
         return xyz

@@ -152,3 +152,38 @@ def fk_closed_form(angles):
     r = 2 * np.cos(t2) + 2 * np.cos(t2 + t3) + 2 * np.cos(t2 + t3 + t4)
     z = 2 + 2 * np.sin(t2) + 2 * np.sin(t2 + t3) + 2 * np.sin(t2 + t3 + t4)
     return np.stack([np.cos(t1) * r, np.sin(t1) * r, z], axis=1)
+
+
+def fk_n(dh, angles):
+    """ForwardKinematics.fkine for any number of features nf >= 4, restated from
+    forward.py:21-94 in numpy: every matrix nf x nf (the 3 x 3 rotations and the
+    translations embedded in the identity, forward.py:42-59), A_i =
+    Rz(theta_i) Tz(d_i) Tx(a_i) Rx(alpha_i) (:63-70), M_{i+1} = M_i A_{i+1} with
+    numpy dot (:85-92).  Returns the list [M_1 .. M_nf] of one angle vector."""
+    dh = np.asarray(dh, np.float64)
+    nf = dh.shape[1]
+
+    def embed(block, rows):
+        m = np.identity(nf)
+        m[:rows, :rows] = block
+        return m
+
+    def rz(t):
+        c, s = np.cos(t), np.sin(t)
+        return embed(np.array([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]]), 3)
+
+    def rx(t):
+        c, s = np.cos(t), np.sin(t)
+        return embed(np.array([[1.0, 0.0, 0.0], [0.0, c, -s], [0.0, s, c]]), 3)
+
+    def tr(v):
+        m = np.identity(nf)
+        m[:3, 3] = v
+        return m
+
+    out = []
+    for i in range(nf):
+        a_i = rz(angles[i]).dot(tr([0.0, 0.0, dh[1, i]])).dot(tr([dh[2, i], 0.0, 0.0])) \
+            .dot(rx(dh[3, i]))
+        out.append(a_i if i == 0 else out[-1].dot(a_i))
+    return out

@@ -566,3 +566,36 @@ def test_ann_tile_variants_agree(ctx1, tmp_path):
     assert r.returncode == 0, r.stderr[-2000:]
     other = np.load(out)
     assert np.array_equal(mine, other["a"]) and np.array_equal(err, other["e"])
+
+
+@pytest.mark.parametrize("nj", [5, 6, 8])
+def test_fk_chains_of_other_lengths(nj):
+    """ForwardKinematics accepts any number of features >= 3 (forward.py:13-19):
+    5..8-joint DH tables on the GPU (ik_fk_chain) against the numpy restatement
+    of forward.py's nf x nf matrices (oracle.fk_n), and 3 features fail like
+    the reference (IndexError, after the angle check)."""
+    from inversekinematicsann_amd.kinematics.forward import ForwardKinematics
+    from inversekinematicsann_amd.robot.robot import OutOfRobotReachException
+    rng = np.random.default_rng(nj)
+    dh = np.vstack([np.zeros(nj), rng.uniform(0, 2, nj), rng.uniform(0, 2, nj),
+                    rng.uniform(-np.pi, np.pi, nj)])
+    fk = ForwardKinematics([list(r) for r in dh])
+    angs = rng.uniform(-np.pi, np.pi, (64, nj))
+    xyz = fk.fkine_batch(angs)
+    for a, p in zip(angs[:8], xyz[:8]):
+        end, mats = fk.fkine(list(a))
+        ref = O.fk_n(dh, a)
+        assert len(mats) == nj and end.shape == (nj, nj)
+        for m, r in zip(mats, ref):
+            assert np.abs(m - r).max() <= 1e-12
+        assert np.abs(p - ref[-1][:3, 3]).max() <= 1e-12
+    bad = angs[0].copy()
+    bad[nj - 1] = 7.0
+    with pytest.raises(OutOfRobotReachException):
+        fk.fkine(list(bad))
+    fk3 = ForwardKinematics([[0.0, 0.0, 0.0], [2.0, 0.0, 0.0], [0.0, 2.0, 2.0],
+                             [np.pi / 2, 0.0, 0.0]])
+    with pytest.raises(IndexError, match="index 3 is out of bounds"):
+        fk3.fkine([0.1, 0.2, 0.3])
+    with pytest.raises(OutOfRobotReachException):
+        fk3.fkine([7.0, 0.2, 0.3])

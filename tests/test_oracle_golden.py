@@ -111,3 +111,13 @@ def test_reference_unit_goldens():
     np.testing.assert_array_almost_equal(xyz, dest, decimal=4)
     # tests/point_unit.py:22,34-37: |(0,0,0)-(-2.22,3.123,0.002)| = 3.831649
     assert abs(math.sqrt(2.22 ** 2 + 3.123 ** 2 + 0.002 ** 2) - 3.831649) < 1e-6
+
+
+def test_oracle_fk_n_pinned_to_reference_fk():
+    """oracle.fk_n (forward.py's nf x nf matrices in numpy, the checker of the
+    5..8-joint FK kernels) reproduces the reference's own 4-joint FK outputs."""
+    g = _load("fk_random.npz")
+    for a, jo in zip(g["angles"][:200], g["joints"][:200]):
+        mats = O.fk_n(O.DH, a)
+        got = np.array([m[:3, 3] for m in mats])
+        assert np.abs(got - jo).max() <= 1e-12
