@@ -202,6 +202,45 @@ def _p99(derr, world):
     return max_over_ranks(float(torch.quantile(fin, 0.99)) if fin.numel() else 0.0, world)
 
 
+_HOST_OUT = {}
+
+
+def _host_out(key, shape, dtype, pinned):
+    """Output arrays of the end-to-end leg, allocated once per shape (pinned or not)."""
+    from inversekinematicsann_amd import _native
+    k = (key, shape, np.dtype(dtype).str, pinned)
+    if k not in _HOST_OUT:
+        _HOST_OUT[k] = _native.pinned_empty(shape, dtype) if pinned else np.empty(shape, dtype)
+    return _HOST_OUT[k]
+
+
+def _host_ann(job, hp, pinned):
+    import ctypes
+    from inversekinematicsann_amd import _native
+    n = hp.shape[0]
+    ang = _host_out("ann_ang", (n, 4), np.float32, pinned)  # the angles only (ann.py:76)
+    s = _native.IkStats()
+    fn = job.ctx.lib.ik_ann_solve_sharded if job.sc is not None else job.ctx.lib.ik_ann_solve
+    job.ctx._check(fn(job.ctx.handle, hp.ctypes.data, n, ang.ctypes.data, None, 0,
+                      ctypes.byref(s)))
+
+
+def _host_fabrik(job, hp, pinned, tol, max_iter):
+    import ctypes
+    from inversekinematicsann_amd import _native
+    n = hp.shape[0]
+    ang = _host_out("fab_ang", (n, 4), np.float64, pinned)  # the angles only (inverse.py:139)
+    s = _native.IkStats()
+    L, h = job.ctx.lib, job.ctx.handle
+    if job.sc is not None:
+        rc = L.ik_fabrik_solve_sharded(h, hp.ctypes.data, n, tol, max_iter, ang.ctypes.data,
+                                       None, None, 0, ctypes.byref(s))
+    else:
+        rc = L.ik_fabrik_solve_fk(h, hp.ctypes.data, n, tol, max_iter, ang.ctypes.data,
+                                  None, None, None, 0, ctypes.byref(s))
+    job.ctx._check(rc)
+
+
 def run_ann(job, args, mode="fp32"):
     import torch
     from inversekinematicsann_amd import _native
@@ -229,9 +268,7 @@ def run_ann(job, args, mode="fp32"):
     res["mean_fk_err"] = sm / job.total
     res["p99_fk_err"] = _p99(derr, world)
     res["outputs"] = {"ang": dang}
-    res["end_to_end"] = end_to_end(
-        job, (lambda hp: job.sc.ann(hp, want_fk_err=True)) if job.sc is not None else
-        (lambda hp: ctx.ann_solve(hp, check_limits=True, want_fk_err=True)), args)
+    res["end_to_end"] = end_to_end(job, lambda hp, pinned: _host_ann(job, hp, pinned), args)
     ctx.ann_set_mode("fp32")
     flop_pt = m.flops_per_point()
     kname = "ann_fused_kernel" if mode == "fp32" else f"ann_fused_kernel_{mode}"
@@ -299,8 +336,7 @@ def run_fabrik(job, args, tol=None, max_iter=None):
     res["p99_fk_err"] = _p99(derr, world)
     res["outputs"] = {"ang": dang, "iters": dit}
     res["end_to_end"] = end_to_end(
-        job, (lambda hp: job.sc.fabrik(hp, tol, max_iter)) if job.sc is not None else
-        (lambda hp: ctx.fabrik_solve(hp, tol, max_iter)), args)
+        job, lambda hp, pinned: _host_fabrik(job, hp, pinned, tol, max_iter), args)
     # this rank's own iterations (the kernel's work), from its shard of the rows
     own = dit[job.lo:job.hi] if job.sc is not None else dit
     local_iters = int(own.sum().item())
@@ -397,23 +433,40 @@ def timed(ctx, step, args, world):
 
 def end_to_end(job, solve_host, args):
     """PCIe-inclusive rate (SURVEY 8(d) "end-to-end"): host float64 points in,
-    host angles out through the library's host-pointer path (H2D, kernels,
-    D2H, stats; with N > 1 the sharded call and its all-gather), pageable numpy
-    buffers.  Reported beside `value`, never as it."""
+    host angles out (the reference's outputs: 24 B in, 16 B (ANN) / 32 B (FABRIK)
+    out per point) through the library's host-pointer path (H2D, kernels, D2H,
+    stats; with N > 1 the sharded call and its all-gather).  Two host memories:
+    pinned (ik_host_alloc; FABRIK: the copies of chunks overlap the kernels of
+    others) and pageable numpy arrays (one shot, the driver stages them).  The
+    box's PCIe moves ~55 GB/s and its two directions do not overlap
+    (tools/pcie_probe.py), so 1M FABRIK points cost >= 1.02 ms of copies.
+    Reported beside `value`, never as it."""
     import torch
+    from inversekinematicsann_amd import _native
     pts = job.pts if job.sc is not None else job.pts[job.lo:job.hi]
     reps = max(1, min(args.steps, 3))
-    solve_host(pts)  # warm the staging scratch
-    barrier(job.world)
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        solve_host(pts)
-    torch.cuda.synchronize()
-    barrier(job.world)
-    wall = max_over_ranks(time.perf_counter() - t0, job.world)
-    ms = wall * 1e3 / reps
+
+    def rate(host_pts, pinned):
+        solve_host(host_pts, pinned)  # warm the staging scratch
+        barrier(job.world)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            solve_host(host_pts, pinned)
+        torch.cuda.synchronize()
+        barrier(job.world)
+        wall = max_over_ranks(time.perf_counter() - t0, job.world)
+        return wall * 1e3 / reps
+
+    pp = _native.pinned_empty(pts.shape, np.float64)
+    pp[:] = pts
+    ms = rate(pp, True)
+    ms_pageable = rate(np.ascontiguousarray(pts), False)
     return {"ms_per_step": ms, "value": job.total / (ms / 1e3), "steps": reps,
-            "unit": "IK solutions/s", "path": "host pointers (ik_*_solve without IK_F_DEVICE)"}
+            "unit": "IK solutions/s",
+            "path": "host pointers (ik_*_solve without IK_F_DEVICE), pinned host arrays "
+                    "(ik_host_alloc; chunked copy/compute overlap)",
+            "pageable": {"ms_per_step": ms_pageable,
+                         "value": job.total / (ms_pageable / 1e3)}}
 
 
 def _host_cpu():

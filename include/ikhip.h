@@ -23,6 +23,7 @@
 #ifndef IKHIP_H
 #define IKHIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -175,6 +176,13 @@ int ik_kernel_times(ik_ctx *ctx, int max, float *ms, char *names, int name_len);
  * count, or -ik_status). */
 int ik_ctx_set_debug(ik_ctx *ctx, int on);
 int ik_debug_read(ik_ctx *ctx, uint64_t *out, int max);
+
+/* Pinned host memory (hipHostMalloc).  A host-pointer FABRIK solve whose arrays
+ * are all pinned and that has at least 131072 points (IKHIP_PIPE_MIN; 0
+ * disables) is cut into chunks whose H2D copies, kernels and D2H copies overlap
+ * on three streams; pageable arrays take the one-shot path. */
+int ik_host_alloc(size_t bytes, void **out);
+int ik_host_free(void *p);
 
 /* After IK_F_ASYNC calls: wait for the stream and read the accumulated stats
  * of the last call. */

@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode",
                     "ik_comm_unique_id", "ik_comm_init", "ik_comm_destroy", "ik_shard_range",
                     "ik_gather_layout_of", "ik_tail_reduce", "ik_ann_solve_sharded",
-                    "ik_fabrik_solve_sharded")
+                    "ik_fabrik_solve_sharded", "ik_host_alloc", "ik_host_free")
 ANN_MODES = {"fp32": 0, "bf16x6": 1, "fp16x3": 2}
 
 
@@ -127,6 +127,8 @@ def load_library(path: str = LIB_PATH):
         L.ik_debug_read.argtypes = [vp, vp, ctypes.c_int]
         L.ik_ann_set_mode.argtypes = [vp, ctypes.c_int]
         L.ik_ann_get_mode.argtypes = [vp]
+        L.ik_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]
+        L.ik_host_free.argtypes = [vp]
         L.ik_comm_unique_id.argtypes = [vp]
         L.ik_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
         L.ik_comm_destroy.argtypes = [vp]
@@ -257,9 +259,9 @@ class Context:
     def fk_device(self, ang, xyz, flags: int = IK_F_DEVICE):
         s = IkStats()
         n = int(ang.shape[0])
-        self._check(self.lib.ik_fk(self.handle, self._dev(ang, "float64", (n, 4), "ang"), n,
-                                   self._dev(xyz, "float64", (n, 3), "xyz"), None, flags,
-                                   ctypes.byref(s)))
+        args = (self._dev(ang, "float64", (n, 4), "ang"), self._dev(xyz, "float64", (n, 3), "xyz"))
+        self._on_torch_stream(lambda: self._check(self.lib.ik_fk(
+            self.handle, args[0], n, args[1], None, flags, ctypes.byref(s))))
         return s
 
     def fabrik_solve(self, pts, tol=1e-3, max_iter=100, check_limits=True,
@@ -292,6 +294,21 @@ class Context:
                                                 _ptr(err), flags, ctypes.byref(s)))
         return ang, it, err, s
 
+    def _on_torch_stream(self, fn):
+        """Run fn with the library on torch's current stream of this device, so a
+        call on tensors that pending torch kernels produce orders after them (the
+        context's own stream does not wait for torch's); the previous stream is
+        restored after.  A caller that pinned a stream with set_stream (bench.py
+        uses one shared stream) gets the same ordering either way."""
+        import torch
+        cur = torch.cuda.current_stream(self.device).cuda_stream
+        prev = self.lib.ik_ctx_get_stream(self.handle)
+        self._check(self.lib.ik_ctx_set_stream(self.handle, cur))
+        try:
+            return fn()
+        finally:
+            self.lib.ik_ctx_set_stream(self.handle, prev)
+
     def _dev(self, t, dtype: str, shape, name: str):
         """Checks a device tensor argument before its pointer goes to the library:
         the kernels read raw memory of a fixed dtype and layout."""
@@ -318,9 +335,9 @@ class Context:
                 self._dev(iters, "int32", (n,), "iters"),
                 self._dev(joints, "float64", (n, 4, 3), "joints"),
                 self._dev(fk_err, "float64", (n,), "fk_err"))
-        self._check(self.lib.ik_fabrik_solve_fk(self.handle, args[0], n, float(tol),
-                                                int(max_iter), args[1], args[2], args[3],
-                                                args[4], flags, ctypes.byref(s)))
+        self._on_torch_stream(lambda: self._check(self.lib.ik_fabrik_solve_fk(
+            self.handle, args[0], n, float(tol), int(max_iter), args[1], args[2], args[3],
+            args[4], flags, ctypes.byref(s))))
         return s
 
     def fabrik_calc(self, dists, init, goals, tol=1e-3, max_iter=100):
@@ -384,10 +401,10 @@ class Context:
     def ann_solve_device(self, pts, ang, fk_err=None, flags: int = IK_F_DEVICE):
         s = IkStats()
         n = int(pts.shape[0])
-        self._check(self.lib.ik_ann_solve(self.handle, self._dev(pts, "float64", (n, 3), "pts"), n,
-                                          self._dev(ang, "float32", (n, 4), "ang"),
-                                          self._dev(fk_err, "float64", (n,), "fk_err"), flags,
-                                          ctypes.byref(s)))
+        args = (self._dev(pts, "float64", (n, 3), "pts"), self._dev(ang, "float32", (n, 4), "ang"),
+                self._dev(fk_err, "float64", (n,), "fk_err"))
+        self._on_torch_stream(lambda: self._check(self.lib.ik_ann_solve(
+            self.handle, args[0], n, args[1], args[2], flags, ctypes.byref(s))))
         return s
 
     # -- multi-GPU (RCCL over xGMI; include/ikhip.h "multi-GPU") -------------
@@ -431,20 +448,22 @@ class Context:
     def ann_solve_sharded_device(self, pts, ang, fk_err=None, flags: int = IK_F_DEVICE):
         s = IkStats()
         n = int(pts.shape[0])
-        self._check(self.lib.ik_ann_solve_sharded(
-            self.handle, self._dev(pts, "float64", (n, 3), "pts"), n,
-            self._dev(ang, "float32", (n, 4), "ang"), self._dev(fk_err, "float64", (n,), "fk_err"),
-            flags, ctypes.byref(s)))
+        args = (self._dev(pts, "float64", (n, 3), "pts"), self._dev(ang, "float32", (n, 4), "ang"),
+                self._dev(fk_err, "float64", (n,), "fk_err"))
+        self._on_torch_stream(lambda: self._check(self.lib.ik_ann_solve_sharded(
+            self.handle, args[0], n, args[1], args[2], flags, ctypes.byref(s))))
         return s
 
     def fabrik_solve_sharded_device(self, pts, ang, iters=None, fk_err=None, tol=1e-3,
                                     max_iter=100, flags: int = IK_F_DEVICE):
         s = IkStats()
         n = int(pts.shape[0])
-        self._check(self.lib.ik_fabrik_solve_sharded(
-            self.handle, self._dev(pts, "float64", (n, 3), "pts"), n, float(tol), int(max_iter),
-            self._dev(ang, "float64", (n, 4), "ang"), self._dev(iters, "int32", (n,), "iters"),
-            self._dev(fk_err, "float64", (n,), "fk_err"), flags, ctypes.byref(s)))
+        args = (self._dev(pts, "float64", (n, 3), "pts"), self._dev(ang, "float64", (n, 4), "ang"),
+                self._dev(iters, "int32", (n,), "iters"), self._dev(fk_err, "float64", (n,),
+                                                                     "fk_err"))
+        self._on_torch_stream(lambda: self._check(self.lib.ik_fabrik_solve_sharded(
+            self.handle, args[0], n, float(tol), int(max_iter), args[1], args[2], args[3], flags,
+            ctypes.byref(s))))
         return s
 
     def set_timing(self, on: bool = True):
@@ -489,6 +508,36 @@ class Context:
 def _host_check(rc: int):
     if rc != IK_OK:
         raise NativeError(rc, load_library().ik_last_error().decode())
+
+
+class _PinnedBlock:
+    """Owner of one ik_host_alloc block; freed when the last array view goes."""
+
+    def __init__(self, nbytes: int):
+        self.lib = load_library()
+        self.ptr = ctypes.c_void_p()
+        _host_check(self.lib.ik_host_alloc(max(1, int(nbytes)), ctypes.byref(self.ptr)))
+        self.nbytes = int(nbytes)
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self.lib.ik_host_free(self.ptr)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def pinned_empty(shape, dtype=np.float64) -> np.ndarray:
+    """A numpy array in pinned host memory (ik_host_alloc): host-pointer solves
+    on such arrays overlap their PCIe copies with the kernels (ikhip.h).  The
+    block is freed when the last view of it goes (the buffer numpy holds keeps
+    its owner alive)."""
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape))
+    blk = _PinnedBlock(n * dt.itemsize)
+    buf = (ctypes.c_char * max(1, n * dt.itemsize)).from_address(blk.ptr.value)
+    buf._owner = blk
+    return np.frombuffer(buf, dtype=dt, count=n).reshape(shape)
 
 
 def comm_unique_id() -> bytes:

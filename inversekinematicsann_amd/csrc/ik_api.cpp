@@ -55,6 +55,7 @@ int fail(int code, const std::string &msg) {
 KtScope::KtScope(ik_ctx *c) {
   g_kt = &c->kt;
   c->kt.n = 0;
+  c->last_stream = c->stream;  // every enqueueing entry point opens one
 }
 KtScope::~KtScope() { g_kt = nullptr; }
 
@@ -114,17 +115,20 @@ namespace ikapi {
 
 // Device pointers only, on the context's stream: stats reset + the kernels.
 int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_iter, double *da,
-                  int32_t *di, double *dj, double *dfe, bool limits, void *work) {
-  launch_reset_stats(c->d_stats, c->stream);
-  launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj, dfe, limits, work,
-                      c->d_stats, c->stream, c->fabrik_variant, c->fabrik_core, c->fab_ord,
-                      c->rconst, c->dbg, c->fabrik_bpc);
+                  int32_t *di, double *dj, double *dfe, bool limits, void *work, DevStats *S) {
+  if (!S) S = c->d_stats;
+  launch_reset_stats(S, c->stream);
+  launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj, dfe, limits, work, S,
+                      c->stream, c->fabrik_variant, c->fabrik_core, c->fab_ord, c->rconst,
+                      c->dbg, c->fabrik_bpc);
   IK_HIP(hipGetLastError());
   return IK_OK;
 }
 
-int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bool limits) {
-  launch_reset_stats(c->d_stats, c->stream);
+int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bool limits,
+               DevStats *S) {
+  if (!S) S = c->d_stats;
+  launch_reset_stats(S, c->stream);
   AnnModelDev m = c->ann;
   m.xmode = c->ann_mode;
   for (int l = 0; l < m.n_layers; ++l) {
@@ -133,7 +137,7 @@ int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bo
                                              : nullptr;
     m.xinv[l] = c->ann_hinv[l];
   }
-  launch_ann(m, c->robot, dp, n, da, de, limits, c->d_stats, c->stream, c->dbg);
+  launch_ann(m, c->robot, dp, n, da, de, limits, S, c->stream, c->dbg);
   IK_HIP(hipGetLastError());
   return IK_OK;
 }
@@ -204,6 +208,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->rconst) (void)hipFree(c->rconst);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   comm_release(c);
+  pipe_release(c);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   for (int i = 0; i < kMaxTimed; ++i) {
     if (c->kt.beg[i]) (void)hipEventDestroy(c->kt.beg[i]);
@@ -316,8 +321,13 @@ int ik_stats_fetch(ik_ctx *c, ik_stats *stats) {
   if (!c) return fail(IK_E_BADARG, "ik_stats_fetch: NULL context");
   int rc = set_dev(c);
   if (rc) return rc;
-  if (c->last_sharded) return sharded_stats(c, stats);
-  return finish(c, 0, stats);
+  // the stats of the last call live on the stream it ran on (ik_ctx_set_stream may
+  // have switched since)
+  hipStream_t cur = c->stream;
+  if (c->last_stream) c->stream = c->last_stream;
+  rc = c->last_sharded ? sharded_stats(c, stats) : finish(c, 0, stats);
+  c->stream = cur;
+  return rc;
 }
 
 int ik_check_limits(ik_ctx *c, const double *pts, int64_t n, int flags, ik_stats *stats) {
@@ -430,6 +440,9 @@ int ik_fabrik_solve_fk(ik_ctx *c, const double *pts, int64_t n, double tol, int3
   if (rc) return rc;
   KtScope kts(c);
   const bool dev = flags & IK_F_DEVICE;
+  if (!dev && pipeline_wanted(c, n, {pts, ang, iters, joints, fk_err}))
+    return fabrik_host_pipeline(c, pts, n, tol, max_iter, ang, iters, joints, fk_err, flags,
+                                stats);
   size_t b_work = Stage::up(fabrik_scratch_bytes(n));
   size_t b_in = dev ? 0 : Stage::up((size_t)n * 24);
   size_t b_ang = dev ? 0 : Stage::up((size_t)n * 32);
@@ -636,6 +649,9 @@ int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk
   if (rc) return rc;
   KtScope kts(c);
   const bool dev = flags & IK_F_DEVICE;
+  // (no chunked pipeline for ANN: its copies are ~2 % of the call and splitting
+  // the launch into chunks costs more tile-quantisation tail than the overlap
+  // saves -- 41.6 vs 41.1 ms per 1M points measured)
   const double *dp = pts;
   float *da = ang;
   double *de = fk_err;

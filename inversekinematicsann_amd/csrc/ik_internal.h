@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <initializer_list>
 #include <string>
 
 #include "ik_common.h"
@@ -33,6 +34,18 @@ struct IkComm {
   hipEvent_t g0 = nullptr, g1 = nullptr;  // around the all-gather
 };
 
+// The chunked host-pointer pipeline (ik_pipe.cpp): copy streams, per-chunk
+// events and stats blocks, device staging; created on first use.
+constexpr int kPipeMaxChunks = 8;
+struct IkPipe {
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  hipEvent_t ev_in[kPipeMaxChunks] = {}, ev_done[kPipeMaxChunks] = {}, ev_out = nullptr;
+  ikhip::DevStats *d_stats = nullptr;  // kPipeMaxChunks blocks
+  ikhip::DevStats *h_stats = nullptr;  // pinned copies
+  void *buf = nullptr;
+  size_t buf_bytes = 0;
+};
+
 struct ik_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -57,6 +70,8 @@ struct ik_ctx {
   ikhip::FabOrderDev *fab_ord = nullptr;  // FABRIK work-order cost table (learned per robot)
   ikhip::RobotConstDev *rconst = nullptr;  // FABRIK seed-pose constants of the robot
   IkComm comm;
+  IkPipe pipe;
+  hipStream_t last_stream = nullptr;  // the stream the last solve was enqueued on
   bool last_sharded = false;  // the last call's stats are in comm.h_tails
   // the gathered tails of the last sharded call (for IK_F_ASYNC + ik_stats_fetch)
   int64_t last_n = 0;
@@ -89,9 +104,19 @@ void stats_from_dev(const ikhip::DevStats &d, ik_stats *s);
 int finish(ik_ctx *c, int flags, ik_stats *stats);
 // Device pointers only, on the context's stream: stats reset + the solve's kernels.
 // work: fabrik_scratch_bytes(n) of device memory.
+// S: the stats block (null: the context's).
 int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_iter, double *da,
-                  int32_t *di, double *dj, double *dfe, bool limits, void *work);
-int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bool limits);
+                  int32_t *di, double *dj, double *dfe, bool limits, void *work,
+                  ikhip::DevStats *S = nullptr);
+int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bool limits,
+               ikhip::DevStats *S = nullptr);
+// FABRIK host-pointer solves whose arrays are all pinned (ik_host_alloc) and large enough:
+// chunked H2D / solve / D2H on three streams (ik_pipe.cpp).
+bool pipeline_wanted(ik_ctx *c, int64_t n, std::initializer_list<const void *> ptrs);
+int fabrik_host_pipeline(ik_ctx *c, const double *pts, int64_t n, double tol, int max_iter,
+                         double *ang, int32_t *iters, double *joints, double *fk_err, int flags,
+                         ik_stats *stats);
+void pipe_release(ik_ctx *c);
 // The batch stats of the last sharded call, from the gathered tails (waits).
 int sharded_stats(ik_ctx *c, ik_stats *stats);
 void comm_release(ik_ctx *c);

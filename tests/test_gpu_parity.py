@@ -599,3 +599,78 @@ def test_fk_chains_of_other_lengths(nj):
         fk3.fkine([0.1, 0.2, 0.3])
     with pytest.raises(OutOfRobotReachException):
         fk3.fkine([7.0, 0.2, 0.3])
+
+
+def test_pinned_host_pipeline_equals_device_path(ctx1):
+    """Host arrays in pinned memory (ik_host_alloc) take the chunked copy / solve /
+    copy pipeline: the same bits as the one-shot pageable path, and the stats of
+    the chunks merge with global indices (an out-of-reach point and a
+    ZeroDivisionError point in different chunks)."""
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER as XS, \
+        REFERENCE_Y_SCALER as YS
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    n = 300_001  # 2 chunks, ragged
+    pts = random_dist(n, seed=41)
+    pts[200_123] = (0.0, 0.0, 2.0)    # ZeroDivisionError, chunk 1
+    pts[250_000] = (1.0, 2.0, -3.5)   # out of reach, chunk 1
+    pts[70_000] = (0.0, 0.0, 2.0)     # ZeroDivisionError, chunk 0
+    pp = _native.pinned_empty((n, 3))
+    pp[:] = pts
+    ang = _native.pinned_empty((n, 4))
+    it = _native.pinned_empty((n,), np.int32)
+    err = _native.pinned_empty((n,), np.float64)
+    s = _native.IkStats()
+    import ctypes
+    rc = ctx1.lib.ik_fabrik_solve_fk(ctx1.handle, pp.ctypes.data, n, 1e-3, 100, ang.ctypes.data,
+                                     it.ctypes.data, None, err.ctypes.data, 0, ctypes.byref(s))
+    assert rc == 0
+    r_ang, r_it, r_err, r_st = ctx1.fabrik_solve_fk(pts, 1e-3, 100)  # pageable: one shot
+    assert np.array_equal(ang, r_ang, equal_nan=True) and np.array_equal(it, r_it)
+    assert np.array_equal(err, r_err, equal_nan=True)
+    for k in ("first_oob", "first_err", "first_err_code", "max_iters", "sum_iters", "n_capped",
+              "max_fk_err"):
+        assert getattr(s, k) == getattr(r_st, k), k
+    assert (s.first_oob, s.first_err) == (250_000, 70_000)
+    m = glorot_model(dims=(3, 64, 64, 4), seed=4)  # ANN on pinned arrays: one shot
+    ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    fa = _native.pinned_empty((n, 4), np.float32)
+    rc = ctx1.lib.ik_ann_solve(ctx1.handle, pp.ctypes.data, n, fa.ctypes.data, err.ctypes.data,
+                               0, ctypes.byref(s))
+    assert rc == 0
+    r_a, r_e, r_s = ctx1.ann_solve(pts, want_fk_err=True)
+    assert np.array_equal(fa, r_a) and np.array_equal(err, r_e, equal_nan=True)
+    assert s.first_oob == r_s.first_oob == 250_000
+
+
+def test_device_tensors_from_pending_torch_ops():
+    """Points produced by a torch kernel still in flight: the device wrappers run
+    the library on torch's current stream, so the solve reads finished inputs;
+    a float32 / non-contiguous / wrong-shape tensor is refused, not misread."""
+    import torch
+    from inversekinematicsann_amd import _native
+    ctx = _native.Context(0)
+    n = 200_000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        base = torch.rand((n, 3), generator=g, dtype=torch.float64, device="cuda")
+        pts = base * torch.tensor([1.5, 2.0, 2.0], dtype=torch.float64, device="cuda") \
+            + torch.tensor([0.2, -1.0, 0.5], dtype=torch.float64, device="cuda")
+        for _ in range(20):  # keep the stream busy so a racing solve would read zeros
+            pts = pts * 1.0
+        ang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
+        it = torch.empty(n, dtype=torch.int32, device="cuda")
+        st = ctx.fabrik_solve_device(pts, ang, it, None, 1e-3, 100)
+        host = pts.cpu().numpy()
+    ref, rit, _, _ = ctx.fabrik_solve(host, 1e-3, 100)
+    assert np.array_equal(ang.cpu().numpy(), ref, equal_nan=True)
+    assert np.array_equal(it.cpu().numpy(), rit) and st.sum_iters == int(rit.sum())
+    with pytest.raises(ValueError, match="dtype"):
+        ctx.fabrik_solve_device(pts.float(), ang)
+    with pytest.raises(ValueError, match="contiguous"):
+        ctx.fabrik_solve_device(pts.t().contiguous().t(), ang)
+    with pytest.raises(ValueError, match="shape"):
+        ctx.fabrik_solve_device(pts, ang[:10])
+    ctx.close()
