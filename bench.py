@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--ann-mode", choices=["fp32", "bf16x6", "fp16x3"], default="fp32",
                     help="ANN hidden-GEMM arithmetic of the headline line (ikhip.h "
                          "ik_ann_set_mode); the other mode is reported under 'secondary'")
+    ap.add_argument("--end-to-end", type=int, default=1,
+                    help="also time the host-pointer (PCIe-inclusive) path; 0 for profiling "
+                         "runs, whose per-kernel averages it would mix in")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01", "pmc"),
                     help="committed PMC diagnosis summaries (pipe occupancy in the roofline)")
@@ -268,7 +271,8 @@ def run_ann(job, args, mode="fp32"):
     res["mean_fk_err"] = sm / job.total
     res["p99_fk_err"] = _p99(derr, world)
     res["outputs"] = {"ang": dang}
-    res["end_to_end"] = end_to_end(job, lambda hp, pinned: _host_ann(job, hp, pinned), args)
+    if args.end_to_end:
+        res["end_to_end"] = end_to_end(job, lambda hp, pinned: _host_ann(job, hp, pinned), args)
     ctx.ann_set_mode("fp32")
     flop_pt = m.flops_per_point()
     kname = "ann_fused_kernel" if mode == "fp32" else f"ann_fused_kernel_{mode}"
@@ -335,8 +339,9 @@ def run_fabrik(job, args, tol=None, max_iter=None):
     res["mean_fk_err"] = sm / job.total
     res["p99_fk_err"] = _p99(derr, world)
     res["outputs"] = {"ang": dang, "iters": dit}
-    res["end_to_end"] = end_to_end(
-        job, lambda hp, pinned: _host_fabrik(job, hp, pinned, tol, max_iter), args)
+    if args.end_to_end:
+        res["end_to_end"] = end_to_end(
+            job, lambda hp, pinned: _host_fabrik(job, hp, pinned, tol, max_iter), args)
     # this rank's own iterations (the kernel's work), from its shard of the rows
     own = dit[job.lo:job.hi] if job.sc is not None else dit
     local_iters = int(own.sum().item())

@@ -33,4 +33,5 @@ PY
 done
 tail -1 $OUT/bench_ann.json > $DST/bench_ann.json
 cp $OUT/traffic.json profiles/traffic.json
+cp $OUT/traffic.json $DST/traffic.json
 ls -la $DST $DST/pmc

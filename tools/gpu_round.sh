@@ -28,9 +28,9 @@ if [ "${PROFILE:-1}" = "1" ]; then
       ann_fp16x3) BARGS="--method ann --ann-mode fp16x3" ;;
       *) BARGS="--method $m" ;;
     esac
-    step prof_stats_$m 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_stats_$m -- python bench.py $BARGS --steps 5 --warmup 1 --cpu-seconds 0 --secondary 0
-    step prof_fetch_$m 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch_$m -- python bench.py $BARGS --steps 2 --warmup 1 --cpu-seconds 0 --secondary 0
-    step prof_write_$m 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write_$m -- python bench.py $BARGS --steps 2 --warmup 1 --cpu-seconds 0 --secondary 0
+    step prof_stats_$m 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_stats_$m -- python bench.py $BARGS --steps 5 --warmup 1 --cpu-seconds 0 --secondary 0 --end-to-end 0
+    step prof_fetch_$m 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/prof_fetch_$m -- python bench.py $BARGS --steps 2 --warmup 1 --cpu-seconds 0 --secondary 0 --end-to-end 0
+    step prof_write_$m 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/prof_write_$m -- python bench.py $BARGS --steps 2 --warmup 1 --cpu-seconds 0 --secondary 0 --end-to-end 0
     python tools/pmc_traffic.py --stats $OUT/prof_stats_$m --fetch $OUT/prof_fetch_$m --write $OUT/prof_write_$m --out $OUT/traffic.json > $OUT/traffic_$m.log 2>&1
   done
 fi

@@ -21,8 +21,12 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = ("ann_fused_kernel", "fabrik_iter_kernel", "fabrik_seed_kernel",
-           "fabrik_angles_kernel", "fabrik_simple_kernel", "fk_kernel")
+KERNELS = ("ann_fused_kernel", "fabrik_iter_kernel", "fabrik_classify_kernel",
+           "fabrik_scatter_kernel", "fabrik_simple_kernel", "reset_stats_kernel",
+           "gather_unpack_kernel", "fk_kernel")
+# every kernel one FABRIK solve launches (ik_fabrik.hip): the pipeline's bytes
+FABRIK_PIPELINE = ("reset_stats_kernel", "fabrik_classify_kernel", "fabrik_scatter_kernel",
+                   "fabrik_iter_kernel")
 
 
 def _short(name: str) -> str | None:
@@ -86,6 +90,12 @@ def main():
             r["fetch_kib_per_launch"] = fk / max(fc, 1)
             r["write_kib_per_launch"] = wk / max(wc, 1)
             r["hbm_bytes_per_launch"] = (2 * fk / max(fc, 1) + wk / max(wc, 1)) * 1024
+    if all(k in fetch and k in write for k in FABRIK_PIPELINE):
+        # per solve: the sum over its launches (60 B per point at the API boundary,
+        # SURVEY 8(d); + 8 B when the FK round-trip errors are written)
+        res["fabrik_pipeline"] = {
+            "kernels": list(FABRIK_PIPELINE),
+            "hbm_bytes_per_launch": sum(res[k]["hbm_bytes_per_launch"] for k in FABRIK_PIPELINE)}
     with open(args.out, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
     print(json.dumps(res, indent=1, sort_keys=True))
