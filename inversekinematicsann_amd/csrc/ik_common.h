@@ -27,10 +27,14 @@ constexpr double kPi = 3.141592653589793;  // math.pi
 constexpr int kStatShards = 64;
 constexpr int kOrdClasses = 16;  // FABRIK work-order cost classes (queue order: hardest first)
 constexpr int kOrdShards = 16;   // ... and the counter shards per class (blocks b % kOrdShards)
+// Work-queue heads of the persistent FABRIK kernel: one returning device-scope
+// atomicAdd on a single word saturates near 88 grabs/us (MI355X_MICROARCH.md,
+// "dequeue"), which 2048 waves grabbing 64-point chunks reach; a head per XCD
+// (blocks b % 8 share one) divides that contention by 8.
+constexpr int kQueueHeads = 8;
 struct DevStats {
   unsigned long long first_oob;      // atomicMin of point index
   unsigned long long first_err_key;  // atomicMin of (index << 8) | code
-  unsigned long long queue;          // work-queue head (persistent kernels)
   unsigned long long ticket;         // blocks of the FABRIK iteration kernel that finished
   // FABRIK work order: points per (cost class, block shard), and the scatter's
   // cursor inside each (class, shard) region of the queue
@@ -41,6 +45,9 @@ struct DevStats {
   unsigned long long max_fk_err_bits[kStatShards];  // atomicMax on non-negative double bits
   double sum_fk_err[kStatShards];
   int max_iters[kStatShards];
+  // the FABRIK iteration kernel's work queue: kQueueHeads heads, one 128-B line
+  // each, head h handing out the queue's chunks h, h + kQueueHeads, ...
+  alignas(128) unsigned long long heads[kQueueHeads][16];
 };
 
 struct d3 {
@@ -508,7 +515,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
                          double *fk_err, bool check_limits, void *scratch, DevStats *S, hipStream_t st,
                          int variant, int core, FabOrderDev *ord, const RobotConstDev *rc,
                          unsigned long long *dbg, int bpc = 0);
-constexpr size_t kFabrikDebugWords = 64 + 4 * 4000;  // diagnostic build counters
+constexpr size_t kFabrikDebugWords = 64 + 24 * 4096;  // diagnostic build: totals + per-wave records
 // Per-robot seed constants (RobotConstDev) into device memory, on stream st.
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t st);
 // The robot constants of the last launch_robot_const, for an unchanged robot.

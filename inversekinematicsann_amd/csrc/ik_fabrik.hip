@@ -246,9 +246,13 @@ struct FabArgs {
 // dbg[64 + 4w ..]: s_memrealtime (100 MHz) at start, when the queue ran dry
 // for it and at the end, and the steps it ran after the queue ran dry.
 enum { kDiagLoops, kDiagSteps, kDiagLaneSteps, kDiagRefills, kDiagGrabs, kDiagFallbacks,
-       kDiagWaves, kDiagFlushes, kDiagFlushTicks, kDiagPrepTicks, kDiagCount };
+       kDiagWaves, kDiagFlushes, kDiagFlushTicks, kDiagPrepTicks, kDiagRefillTicks,
+       kDiagParkTicks, kDiagStageTicks, kDiagCount };
+// per-wave record (kDiagWords): the counters above, then s_memrealtime stamps
+enum { kDiagTStart = kDiagCount, kDiagTDry, kDiagTLast, kDiagStepsDry, kDiagTDrain, kDiagTEnd,
+       kDiagTRefill, kDiagTSub, kDiagWords = 24 };
 #ifdef IKHIP_DIAG
-constexpr int kDiagWaveMax = 4000;  // = (kFabrikDebugWords - 64) / 4
+constexpr int kDiagWaveMax = 4096;  // = (kFabrikDebugWords - 64) / kDiagWords (24)
 #endif
 
 static int env_int(const char *name, int dflt) {
@@ -296,6 +300,7 @@ __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const 
   acc.sum_it += (unsigned long long)it;
   acc.capped += (it >= a.max_iter) ? 1ull : 0ull;
   acc.max_it = max(acc.max_it, it);
+#ifndef IKHIP_EXP_NOFK
   if (a.fk_err) {
     double e = __builtin_nan("");
     if (st == IK_OK) {
@@ -311,6 +316,7 @@ __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const 
       acc.fk_sum += e;
     }
   }
+#endif
 }
 
 // ------------------------------------------------------------- simple ----
@@ -553,8 +559,13 @@ __device__ __forceinline__ d3 shfl3(const d3 v, int src) {
 // distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
 // Every solve reaching this kernel runs at least one iteration (the host sends
 // the others to fabrik_simple_kernel), so the seed's last joint is never needed.
+#ifndef IKHIP_ITER_WAVES
+#define IKHIP_ITER_WAVES 2
+#endif
+constexpr int kIterWaves = IKHIP_ITER_WAVES;  // waves per SIMD = blocks per CU
 template <int REFILL_MIN, bool ORD, int CORE>
-__global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kIterWaves, kIterWaves))) void
+fabrik_iter_kernel(FabArgs a) {
   __shared__ RetireRing rings[4];
   const int lane = threadIdx.x & 63;
   RetireRing &R = rings[threadIdx.x >> 6];
@@ -572,6 +583,12 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   // permutation entries loaded (nperm), 3 its goals loaded (ng, ni); -1 the queue is dry
   int nstage = 0, ncount = 0;
   int64_t nbase = 0;
+  // the queue head this wave grabs from (its block's, blockIdx % kQueueHeads,
+  // until that one runs dry; then the next one its block has not seen dry)
+  __shared__ unsigned int dry_heads;  // the heads this block found dry
+  if (threadIdx.x == 0) dry_heads = 0;
+  __syncthreads();
+  int head = (int)(blockIdx.x % kQueueHeads);
   unsigned long long na = 0;
   int64_t nperm = 0, ni = 0;
   d3 ng = {0, 0, 0};
@@ -589,12 +606,29 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
   uint32_t cdom = 0;
 
 #ifdef IKHIP_DIAG
-  unsigned long long dg[kDiagCount] = {};
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-  unsigned long long t_dry = 0, steps_dry = 0;
-#define IKHIP_DG(k, v) (dg[k] += (v))
+  // counters and stamps live in LDS (lane 0 writes), so that the diagnostic
+  // build keeps the production kernel's registers and occupancy
+  __shared__ unsigned long long dgs[4][kDiagWords];
+  unsigned long long *dg = dgs[threadIdx.x >> 6];
+  if (lane < kDiagWords) dg[lane] = 0;
+  __builtin_amdgcn_wave_barrier();
+  if (lane == 0) dg[kDiagTStart] = __builtin_amdgcn_s_memrealtime();
+#define IKHIP_DG(k, v) \
+  do {                 \
+    if (lane == 0) dg[k] += (v); \
+  } while (0)
+#define IKHIP_DT(k) \
+  do {              \
+    if (lane == 0) dg[k] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define IKHIP_DT_ACC(k, k0) \
+  do {                      \
+    if (lane == 0) dg[k] += __builtin_amdgcn_s_memrealtime() - dg[k0]; \
+  } while (0)
 #else
 #define IKHIP_DG(k, v) ((void)0)
+#define IKHIP_DT(k) ((void)0)
+#define IKHIP_DT_ACC(k, k0) ((void)0)
 #endif
   while (true) {
     const unsigned long long freem = __ballot(!active);
@@ -603,36 +637,51 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
     IKHIP_DG(kDiagLoops, 1);
     if (!dry && (nfree >= REFILL_MIN || nfree == 64)) {
       IKHIP_DG(kDiagRefills, 1);
+      IKHIP_DT(kDiagTRefill);  // refill time, less the flushes and preparations in it
+      IKHIP_DT(kDiagTSub);
       // park the lanes that finished since the last refill
       const unsigned long long pm = __ballot(pending);
       const int np = __popcll(pm);
       if (np) {
         if (rcnt + np > 64) {
           IKHIP_DG(kDiagFlushes, 1);
-#ifdef IKHIP_DIAG
-          const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
-#endif
+          IKHIP_DT(kDiagTEnd);  // (scratch slot: the flush's start)
           ring_flush<ORD>(a, R, rcnt, lane, acc);
-#ifdef IKHIP_DIAG
-          dg[kDiagFlushTicks] += __builtin_amdgcn_s_memrealtime() - tf0;
-#endif
+          IKHIP_DT_ACC(kDiagFlushTicks, kDiagTEnd);
+          IKHIP_DT_ACC(kDiagTRefill, kDiagTEnd);  // (not refill time)
           rcnt = 0;
         }
         if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, out, step, st);
         pending = false;
         rcnt += np;
       }
+      IKHIP_DT_ACC(kDiagParkTicks, kDiagTSub);
+      IKHIP_DT(kDiagTSub);
       // the next batch's stages, one per refill while the last 24 entries of this
       // one are handed out; a stage consumes what the one before loaded (so the
       // loads are long done), and prepare() runs the stages still missing
       auto stage1 = [&]() {
-        if (lane == 0) na = atomicAdd(&a.S->queue, (unsigned long long)a.chunk);
+        if (lane == 0) na = atomicAdd(&a.S->heads[head][0], 1ull);
         nstage = 1;
       };
       auto stage2 = [&]() {
-        nbase = (int64_t)__shfl(na, 0, 64);
-        if (nbase >= a.n) {
-          nstage = -1;
+        // the grab's chunk: head h's k-th is the queue's (k * kQueueHeads + h)-th
+        nbase = ((int64_t)__shfl(na, 0, 64) * kQueueHeads + head) * a.chunk;
+        if (nbase >= a.n) {  // this head is dry: on to one the block has not seen dry
+          if (lane == 0) atomicOr(&dry_heads, 1u << head);
+          const unsigned m =
+              __builtin_amdgcn_readfirstlane(__hip_atomic_load(&dry_heads, __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP)) |
+              (1u << head);
+          if (m == (1u << kQueueHeads) - 1) {
+            nstage = -1;
+            return;
+          }
+          int h = head;
+          do h = (h + 1) % kQueueHeads;
+          while ((m >> h) & 1u);
+          head = h;
+          nstage = 0;
           return;
         }
         ncount = (int)min((int64_t)a.chunk, a.n - nbase);
@@ -649,6 +698,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
       if (nstage == 0 && pptr >= pcount - 24) stage1();
       else if (nstage == 1 && pptr >= pcount - 16) stage2();
       else if (nstage == 2 && pptr >= pcount - 8) stage3();
+      IKHIP_DT_ACC(kDiagStageTicks, kDiagTSub);
       // hand prepared points to the free lanes, preparing batches as needed
       const bool wasfree = !active;
       const int rank = __popcll(freem & lt_mask);
@@ -656,12 +706,12 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
       while (handed < nfree) {
         if (pptr >= pcount) {
           IKHIP_DG(kDiagGrabs, 1);
-#ifdef IKHIP_DIAG
-          const unsigned long long tp0 = __builtin_amdgcn_s_memrealtime();
-#endif
-          if (nstage == 0) stage1();
-          if (nstage == 1) stage2();
-          if (nstage == 2) stage3();
+          IKHIP_DT(kDiagTDrain);  // (scratch slot: the preparation's start)
+          while (nstage >= 0 && nstage < 3) {  // (stage2 may send it back to 0)
+            if (nstage == 0) stage1();
+            else if (nstage == 1) stage2();
+            else stage3();
+          }
           if (nstage < 0) break;
           // prepare: limits check and seed pose of the batch, one entry per lane
           pcount = ncount;
@@ -686,8 +736,9 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
 #ifdef IKHIP_DIAG
           // (the seed's loads are consumed before the stamp)
           asm volatile("" ::"v"(P0.x), "v"(P1.x), "v"(P2.x), "v"(Pg.x));
-          dg[kDiagPrepTicks] += __builtin_amdgcn_s_memrealtime() - tp0;
 #endif
+          IKHIP_DT_ACC(kDiagPrepTicks, kDiagTDrain);
+          IKHIP_DT_ACC(kDiagTRefill, kDiagTDrain);  // (not refill time)
         }
         const int take = min(nfree - handed, pcount - pptr);
         const bool mine = wasfree && rank >= handed && rank < handed + take;
@@ -712,17 +763,19 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
         handed += take;
       }
       dry = nstage < 0 && pptr >= pcount;
+      IKHIP_DT_ACC(kDiagRefillTicks, kDiagTRefill);
     }
 #ifdef IKHIP_DIAG
     {
       const unsigned long long sm =
           __ballot(active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step));
-      dg[kDiagSteps] += sm ? 1 : 0;
-      dg[kDiagLaneSteps] += __popcll(sm);
-      if (nstage < 0) {
-        if (!t_dry) t_dry = __builtin_amdgcn_s_memrealtime();
-        steps_dry += sm ? 1 : 0;
+      IKHIP_DG(kDiagSteps, sm ? 1 : 0);
+      IKHIP_DG(kDiagLaneSteps, __popcll(sm));
+      if (dry) {  // the queue and the wave's batch are exhausted
+        if (lane == 0 && dg[kDiagTDry] == 0) dg[kDiagTDry] = __builtin_amdgcn_s_memrealtime();
+        IKHIP_DG(kDiagStepsDry, sm ? 1 : 0);
       }
+      if (sm) IKHIP_DT(kDiagTLast);
     }
 #endif
     if (active) {
@@ -771,6 +824,7 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
     }
   }
   // drain: park the last finished lanes, then the angles step on the ring
+  IKHIP_DT(kDiagTDrain);
   {
     const unsigned long long pm = __ballot(pending);
     const int np = __popcll(pm);
@@ -781,28 +835,23 @@ __global__ __launch_bounds__(256) void fabrik_iter_kernel(FabArgs a) {
     if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, out, step, st);
     rcnt += np;
     IKHIP_DG(kDiagFlushes, 1);
-#ifdef IKHIP_DIAG
-    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
-#endif
+    IKHIP_DT(kDiagTEnd);
     ring_flush<ORD>(a, R, rcnt, lane, acc);
-#ifdef IKHIP_DIAG
-    dg[kDiagFlushTicks] += __builtin_amdgcn_s_memrealtime() - tf0;
-#endif
+    IKHIP_DT_ACC(kDiagFlushTicks, kDiagTEnd);
   }
 #ifdef IKHIP_DIAG
-  if (a.dbg && lane == 0) {
-    dg[kDiagWaves] = 1;
-    for (int k = 0; k < kDiagCount; ++k) atomicAdd(&a.dbg[k], dg[k]);
+  IKHIP_DT(kDiagTEnd);
+  IKHIP_DG(kDiagWaves, 1);
+  __builtin_amdgcn_wave_barrier();
+  if (a.dbg) {
     const int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-    if (w < kDiagWaveMax) {
-      a.dbg[64 + 4 * w] = t_start;
-      a.dbg[65 + 4 * w] = t_dry;
-      a.dbg[66 + 4 * w] = __builtin_amdgcn_s_memrealtime();
-      a.dbg[67 + 4 * w] = steps_dry;
-    }
+    if (lane < kDiagCount) atomicAdd(&a.dbg[lane], dg[lane]);
+    if (w < kDiagWaveMax && lane < kDiagWords) a.dbg[64 + kDiagWords * w + lane] = dg[lane];
   }
 #endif
 #undef IKHIP_DG
+#undef IKHIP_DT
+#undef IKHIP_DT_ACC
   block_iter_stats_acc(a.S, acc.sum_it, acc.capped, acc.max_it);
   if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
   if constexpr (ORD) {
@@ -924,7 +973,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   // bpc_req: the context's IKHIP_FABRIK_BPC (0 = this rule)
   // The fused kernel keeps the batch of prepared points and the angles step's
   // temporaries beside the loop state: ~250 VGPRs, two waves per SIMD at most.
-  const int bpc = bpc_req > 0 ? (bpc_req < 2 ? bpc_req : 2) : 2;
+  const int bpc = bpc_req > 0 ? (bpc_req < kIterWaves ? bpc_req : kIterWaves) : kIterWaves;
   static const int chunk = env_int("IKHIP_FABRIK_CHUNK", 64);
   a.chunk = (chunk > 0 && chunk <= 64) ? chunk : 64;
   unsigned pgrid = (unsigned)num_cus() * (unsigned)(bpc > 0 ? bpc : 8);

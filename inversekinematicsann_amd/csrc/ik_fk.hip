@@ -14,9 +14,9 @@ __global__ void reset_stats_kernel(DevStats *S) {
   if (t == 0) {
     S->first_oob = ~0ull;
     S->first_err_key = ~0ull;
-    S->queue = 0;
     S->ticket = 0;
   }
+  if (t < kQueueHeads) S->heads[t][0] = 0;
   for (int e = t; e < kOrdClasses * kOrdShards; e += blockDim.x) {
     (&S->cls_tot[0][0])[e] = 0;
     (&S->cls_cur[0][0])[e] = 0;

@@ -16,7 +16,9 @@ os.environ.setdefault("IKHIP_LIB", os.path.join(ROOT, "inversekinematicsann_amd"
 from inversekinematicsann_amd import _native  # noqa: E402
 from inversekinematicsann_amd.robot.position_generator import random_dist  # noqa: E402
 
-NAMES = ["loops", "steps", "lane_steps", "refills", "grabs", "fallbacks", "waves", "flushes", "flush_ticks", "prep_ticks"]
+NAMES = ["loops", "steps", "lane_steps", "refills", "grabs", "fallbacks", "waves", "flushes",
+         "flush_ticks", "prep_ticks", "refill_ticks", "park_ticks", "stage_ticks"]
+REC = 24  # words per wave record (ik_fabrik.hip kDiagWords)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 pts = torch.from_numpy(random_dist(n, seed=0)).cuda()
 ang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
@@ -28,23 +30,39 @@ for tol, mi in ((1e-3, 100), (1e-5, 200)):
         ctx.fabrik_solve_device(pts, ang, it, None, tol, mi, flags=_native.IK_F_DEVICE)
     ctx.set_debug(True)
     ctx.fabrik_solve_device(pts, ang, it, None, tol, mi, flags=_native.IK_F_DEVICE)
-    w = ctx.debug_words(64 + 4 * 4000).astype(np.int64)
+    w = ctx.debug_words(64 + REC * 4096).astype(np.int64)
     ctx.set_debug(False)
     c = dict(zip(NAMES, w[:len(NAMES)].tolist()))
-    nw = min(c["waves"], 4000)
-    t = w[64:64 + 4 * nw].reshape(nw, 4)
-    t0 = t[:, 0].min()
-    us = lambda v: np.percentile((v - t0) / 100.0, [0, 1, 10, 50, 90, 99, 100]).round(1).tolist()
+    nw = min(c["waves"], 4096)
+    t = w[64:64 + REC * nw].reshape(nw, REC)
+    # per-wave record: the counters, then start, dry, last step, steps after
+    # dry, drain, end (s_memrealtime, 100 MHz)
+    T0, TDRY, TLAST, SDRY, TDRAIN, TEND = range(len(NAMES), len(NAMES) + 6)
+    t0 = t[:, T0].min()
+    pc = [0, 1, 10, 50, 90, 99, 100]
+    us = lambda v: np.percentile((v - t0) / 100.0, pc).round(1).tolist()
+    span = lambda a, b: np.percentile((t[:, b] - t[:, a]) / 100.0, pc).round(2).tolist()
     c["lane_eff"] = c["lane_steps"] / (64.0 * max(c["steps"], 1))
     c["sum_iters"] = int(it.sum().item())
+    c["steps_per_refill"] = c["steps"] / max(c["refills"], 1)
     c["flush_us_per_wave"] = c["flush_ticks"] / 100.0 / max(c["waves"], 1)
     c["prep_us_per_wave"] = c["prep_ticks"] / 100.0 / max(c["waves"], 1)
-    c["steps_per_refill"] = c["steps"] / max(c["refills"], 1)
-    c["pct"] = [0, 1, 10, 50, 90, 99, 100]
-    c["wave_start_us"] = us(t[:, 0])
-    c["wave_dry_us"] = us(t[:, 1])
-    c["wave_end_us"] = us(t[:, 2])
-    c["steps_after_dry"] = np.percentile(t[:, 3], [0, 1, 10, 50, 90, 99, 100]).tolist()
-    c["us_per_step_after_dry"] = float(((t[:, 2] - t[:, 1]) / 100.0).sum() / max(t[:, 3].sum(), 1))
+    for k in ("refill", "park", "stage"):
+        c[k + "_us_per_wave"] = c[k + "_ticks"] / 100.0 / max(c["waves"], 1)
+    c["pct"] = pc
+    c["wave_start_us"] = us(t[:, T0])
+    c["wave_dry_us"] = us(t[:, TDRY])       # queue and the wave's batch exhausted
+    c["wave_last_step_us"] = us(t[:, TLAST])
+    c["wave_drain_us"] = us(t[:, TDRAIN])   # loop left
+    c["wave_end_us"] = us(t[:, TEND])       # after the final angles step
+    c["steps_after_dry"] = np.percentile(t[:, SDRY], pc).tolist()
+    c["dry_to_last_step_us"] = span(TDRY, TLAST)
+    c["last_step_to_drain_us"] = span(TLAST, TDRAIN)
+    c["drain_to_end_us"] = span(TDRAIN, TEND)
+    c["wave_us"] = span(T0, TEND)
+    # busy waves over time (10 us bins): how the launch drains
+    edges = np.arange(0, (t[:, TEND].max() - t0) / 100.0 + 10, 10)
+    c["waves_running_10us"] = [int(((t[:, T0] - t0) / 100.0 <= e).sum() -
+                                   ((t[:, TEND] - t0) / 100.0 <= e).sum()) for e in edges]
     out[f"tol{tol:g}"] = c
 print(json.dumps(out, indent=1))
