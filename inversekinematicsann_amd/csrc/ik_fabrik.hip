@@ -283,8 +283,8 @@ __device__ __forceinline__ bool outside_rc(RcConst k, d3 g) {
   return outside(lim, g.x, g.y, g.z);
 }
 
-__device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const d3 J[4], int it,
-                                             int st, LaneAcc &acc) {
+__device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const d3 J[4], d3 g,
+                                             int it, int st, LaneAcc &acc) {
   double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
 #ifndef IKHIP_EXP_NOANGLES
   if (st == IK_OK) get_angles(J, th, st);
@@ -308,7 +308,7 @@ __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const 
       double jc[16];
 #pragma unroll
       for (int e2 = 0; e2 < 16; ++e2) jc[e2] = k->jc[e2];
-      e = fk_error(jc, th, a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2], k->alpha_bad);
+      e = fk_error(jc, th, g.x, g.y, g.z, k->alpha_bad);
     }
     a.fk_err[i] = e;
     if (e == e) {
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
         if (st != IK_OK) break;
       }
     }
-    finish_point(a, i, J, it, st, acc);
+    finish_point(a, i, J, g, it, st, acc);
   }
   block_iter_stats_acc(a.S, acc.sum_it, acc.capped, acc.max_it);
   if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
@@ -510,18 +510,20 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
 // the handful of lanes that finish together.
 struct RetireRing {
   double j[12][64];
+  double g[3][64];  // the goal, for the FK round trip (not read from HBM again)
   long long idx[64];
   int it[64];
   int st[64];
 };
 
 __device__ __forceinline__ void ring_put(RetireRing &R, int s, const d3 &J0, const d3 &J1,
-                                         const d3 &J2, const d3 &J3, int64_t idx, int it,
-                                         int st) {
+                                         const d3 &J2, const d3 &J3, const d3 &g, int64_t idx,
+                                         int it, int st) {
   R.j[0][s] = J0.x; R.j[1][s] = J0.y; R.j[2][s] = J0.z;
   R.j[3][s] = J1.x; R.j[4][s] = J1.y; R.j[5][s] = J1.z;
   R.j[6][s] = J2.x; R.j[7][s] = J2.y; R.j[8][s] = J2.z;
   R.j[9][s] = J3.x; R.j[10][s] = J3.y; R.j[11][s] = J3.z;
+  R.g[0][s] = g.x; R.g[1][s] = g.y; R.g[2][s] = g.z;
   R.idx[s] = idx;
   R.it[s] = it;
   R.st[s] = st;
@@ -540,7 +542,7 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
       J[k] = {R.j[3 * k][lane], R.j[3 * k + 1][lane], R.j[3 * k + 2][lane]};
     const int64_t i = R.idx[lane];
     const int it = R.it[lane];
-    finish_point(a, i, J, it, R.st[lane], acc);
+    finish_point(a, i, J, {R.g[0][lane], R.g[1][lane], R.g[2][lane]}, it, R.st[lane], acc);
     if constexpr (ORD) {
       if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
         a.ord->sample[i / kOrdSample] = ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) |
@@ -651,7 +653,7 @@ fabrik_iter_kernel(FabArgs a) {
           IKHIP_DT_ACC(kDiagTRefill, kDiagTEnd);  // (not refill time)
           rcnt = 0;
         }
-        if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, out, step, st);
+        if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, g, out, step, st);
         pending = false;
         rcnt += np;
       }
@@ -832,7 +834,7 @@ fabrik_iter_kernel(FabArgs a) {
       ring_flush<ORD>(a, R, rcnt, lane, acc);
       rcnt = 0;
     }
-    if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, out, step, st);
+    if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, g, out, step, st);
     rcnt += np;
     IKHIP_DG(kDiagFlushes, 1);
     IKHIP_DT(kDiagTEnd);
