@@ -485,7 +485,18 @@ def _host_cpu():
                     break
     except OSError:
         pass
-    return {"model": model, "os_cpu_count": os.cpu_count()}
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": affinity,
+            "omp_num_threads": omp,
+            # why `cores` is not os_cpu_count: a one-GPU box is leased one GPU's share of
+            # the host (OMP_NUM_THREADS, set by the box), and the baseline uses that share
+            "cores_note": ("one GPU's share of the host: OMP_NUM_THREADS=%s on this box; "
+                           "os.cpu_count() counts the whole machine" % omp) if omp else
+                          "all CPUs this process may use"}
 
 
 # cpu_baseline samples: the first points of the GPU batch, which the oracle's output on

@@ -23,6 +23,7 @@
 // The grid is persistent: workgroups walk the point tiles.
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 
 #include "ik_common.h"
 
@@ -518,6 +519,19 @@ __device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__res
   if (g + 1 < G16) step_x<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
 }
 
+// Compile-time loop: f(std::integral_constant<int, 0>) .. f(<N - 1>).
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_(F &&f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_<I + 1, N>(f);
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+  static_for_<0, N>(f);
+}
+
 // ------------------------------------------------- split-fp16 (fp16x3) mode ----
 // Opt-in (IK_ANN_FP16X3): x = hi + lo in fp16 (round to nearest; the residual
 // is exact in fp32), weights pre-scaled by 2^k so their largest is ~2^14, and
@@ -568,12 +582,20 @@ __device__ __forceinline__ void load_wh(WStepH<NR> &w, const WStream<NR> &ws, in
 
 // One K step (see step_x): weights of step g+2 and A of step g+1 in the shadow
 // of the 3 * MR * NR MFMAs of step g.
+#ifndef IKHIP_ANN_XRING
+#define IKHIP_ANN_XRING 3
+#endif
+// fp16x3 weight-step buffers (kXRing - 1 steps ahead).  4, 5 and 6 buffers
+// (no spills; AGPRs 136 -> 232) measured 15.66 / 15.84 / 15.77 ms against 15.50
+// for 3 at 1M points (tools/ann_ab.sh): the weight stream is not latency-bound
+// but at the L2's rate for a table every CU reads (DESIGN.md "fp16x3").
+constexpr int kXRing = IKHIP_ANN_XRING;
 template <int MR, int NR, int GI>
 __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WStepH<NR> &fill,
                                        const WStream<NR> &ws, const float *ab, int g,
                                        f32x16 (&acc)[MR][NR]) {
   __builtin_amdgcn_sched_barrier(0);
-  load_wh(fill, ws, g + 2);
+  load_wh(fill, ws, g + kXRing - 1);
   f32x8 an[MR];
   load_a(an, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
   Split2 sn[MR];
@@ -611,9 +633,9 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
   const float *ap = H + r * kLd + 8 * h;
   acc_init_bias(acc, bias, wave, kWaves, lane, 1.0f / xinv);  // exact: xinv is 2^-k
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 2, lane);
-  WStepH<NR> w0, w1, w2;
-  load_wh(w0, ws, 0);
-  load_wh(w1, ws, 1);
+  WStepH<NR> w[kXRing];
+#pragma unroll
+  for (int u = 0; u < kXRing - 1; ++u) load_wh(w[u], ws, u);
   Split2 sa[MR];
   {
     f32x8 a0[MR];
@@ -622,15 +644,19 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
     for (int m = 0; m < MR; ++m) sa[m] = split2h(a0[m]);
   }
   int g = 0;
-  for (; g + 3 <= G16; g += 3) {
+  for (; g + kXRing <= G16; g += kXRing) {
     const float *ab = ap + 16 * g;
-    step_h<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
-    step_h<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
-    step_h<MR, NR, 2>(sa, w2, w1, ws, ab, g + 2, acc);
+    static_for<kXRing>([&](auto u) {
+      step_h<MR, NR, u.value>(sa, w[u.value], w[(u.value + kXRing - 1) % kXRing], ws, ab,
+                              g + u.value, acc);
+    });
   }
   const float *ab = ap + 16 * g;
-  if (g < G16) step_h<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
-  if (g + 1 < G16) step_h<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
+  static_for<kXRing - 1>([&](auto u) {
+    if (g + u.value < G16)
+      step_h<MR, NR, u.value>(sa, w[u.value], w[(u.value + kXRing - 1) % kXRing], ws, ab,
+                              g + u.value, acc);
+  });
 #pragma unroll
   for (int m = 0; m < MR; ++m)
 #pragma unroll
