@@ -67,7 +67,7 @@ def parse():
                     help="also time the host-pointer (PCIe-inclusive) path; 0 for profiling "
                          "runs, whose per-kernel averages it would mix in")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r01", "pmc"),
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r02", "pmc"),
                     help="committed PMC diagnosis summaries (pipe occupancy in the roofline)")
     ap.add_argument("--gather", type=int, default=1,
                     help="N>1: the sharded solve with the library's RCCL all-gather of every "
@@ -291,9 +291,8 @@ def run_ann(job, args, mode="fp32"):
                        "traffic": traffic, "kernel": kname,
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
                        "points_per_launch": n}
-    if mode == "fp32":
-        res["roofline"]["pipes"] = load_pipe(os.path.join(args.pmc_dir, "ann_diag_summary.json"),
-                                             "ann_fused_kernel")
+    diag = "ann_diag_summary.json" if mode == "fp32" else f"ann_{mode}_diag_summary.json"
+    res["roofline"]["pipes"] = load_pipe(os.path.join(args.pmc_dir, diag), "ann_fused_kernel")
     if mode == "fp32":
         res["dtype"] = "fp32"
         res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
