@@ -572,8 +572,12 @@ fabrik_iter_kernel(FabArgs a) {
   const int lane = threadIdx.x & 63;
   RetireRing &R = rings[threadIdx.x >> 6];
   const unsigned long long lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const double tol2 = a.tol2;
-  const int max_iter = a.max_iter;
+  // the loop condition's operands held in VGPRs: as wave-uniform values they
+  // compete for the SGPRs the nested exec masks need, and the compiler then
+  // re-read tol2 from the kernel arguments (s_load + wait) every iteration
+  double tol2 = a.tol2;
+  int max_iter = a.max_iter;
+  asm volatile("" : "+v"(tol2), "+v"(max_iter));
   double L[4] = {a.r.links[0], a.r.links[1], a.r.links[2], a.r.links[3]};
 
   // prepared points: lane j holds the batch's entry j (wave-uniform count / cursor)
