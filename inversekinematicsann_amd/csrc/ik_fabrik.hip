@@ -784,8 +784,13 @@ fabrik_iter_kernel(FabArgs a) {
       if (sm) IKHIP_DT(kDiagTLast);
     }
 #endif
-    if (active) {
-      if (st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step)) {
+    {
+      // one divergent region per iteration: lanes that stop here become pending
+      // (parked at the next refill) without a branch of their own
+      const bool run = active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step);
+      pending = pending || (active && !run);
+      active = run;
+      if (run) {
         if constexpr (CORE == 2) {
           uint32_t dom = 0, cdom_n = cdom;
           d3 n1 = J1, n2 = J2, n3 = J3, cd_n = cd;
@@ -823,9 +828,6 @@ fabrik_iter_kernel(FabArgs a) {
           fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
         }
         ++step;
-      } else {
-        active = false;
-        pending = true;
       }
     }
   }
