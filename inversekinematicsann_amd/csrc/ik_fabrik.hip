@@ -97,14 +97,15 @@ __device__ __forceinline__ void fabrik_step4_reuse(const d3 start, d3 &c1, d3 &c
 
 // The carry of fabrik_step4_reuse for a chain whose c2 did not come from it (a
 // refilled lane's seed pose, or the general step of a fallback), through the
-// general sqrt / division: the same bits inside sqrt_core's domain, and outside it
-// cdom sends the next iteration to the fallback, which recomputes everything.
+// core sequences: inside sqrt_core's domain they are the general sqrt / division's
+// bits, and outside it cdom sends the next iteration to the fallback, which
+// recomputes everything without reading cq (so the value is never used there).
 __device__ __forceinline__ void reuse_carry(const d3 c2, const d3 g, double L3, double &cq,
                                             d3 &cd, uint32_t &cdom) {
   cd = {g.x - c2.x, g.y - c2.y, g.z - c2.z};
   const double x = sq(cd.x) + sq(cd.y) + sq(cd.z);
   cdom = sqrt_core_dom(x);
-  cq = L3 / sqrt(x);
+  cq = div_core(L3, sqrt_core(x));
 }
 
 // div_core's domain for the link lengths (the numerators): 2^-100 <= |L| <= 2^100.
