@@ -306,6 +306,36 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
     if (g + u < g1) mma_group<MR, NR, TR>(f[u], acc);
 }
 
+// fp16x3 activation planes.  A layer whose successor runs in fp16x3 stores its
+// activations already split, x = hi + lo in fp16 (the residual exact in fp32),
+// row r of H holding the 512 hi halves in bytes [0, 1024) and the 512 lo halves
+// in [1024, 2048) of its 2064: the next layer's K loop then reads its operands
+// with no conversion, and each activation is split once by the wave that wrote it
+// instead of once by every wave that reads it (4x), in the MFMA loop.
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ _Float16 *hplane(float *H, int row) {
+  return reinterpret_cast<_Float16 *>(H + row * kLd);
+}
+
+__device__ __forceinline__ void store_h4(float *H, int row, int col, f32x4 v) {
+  const f32x2 v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
+  const f16x2 h01 = __builtin_convertvector(v01, f16x2), h23 = __builtin_convertvector(v23, f16x2);
+  const f16x2 l01 = __builtin_convertvector(v01 - __builtin_convertvector(h01, f32x2), f16x2);
+  const f16x2 l23 = __builtin_convertvector(v23 - __builtin_convertvector(h23, f32x2), f16x2);
+  _Float16 *p = hplane(H, row) + col;
+  *reinterpret_cast<f16x4 *>(p) = f16x4{h01[0], h01[1], h23[0], h23[1]};
+  *reinterpret_cast<f16x4 *>(p + 512) = f16x4{l01[0], l01[1], l23[0], l23[1]};
+}
+
+__device__ __forceinline__ void store_h1(float *H, int row, int col, float v) {
+  const _Float16 h = (_Float16)v;
+  _Float16 *p = hplane(H, row) + col;
+  p[0] = h;
+  p[512] = (_Float16)(v - (float)h);
+}
+
 // Epilogue of a full-width fp32 layer (C layout: column lane & 31, rows
 // (q & 3) + 8 (q >> 2) + 4 (lane >> 5)).  bv[j]: the bias of the lane's column
 // in tile j, loaded before the GEMM (a load issued here, after the barrier,
@@ -313,7 +343,7 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
 // transposed form below (bias in the accumulators, b128 stores) measured
 // 0.6 k cycles per layer slower here: its 5.9 k-cycle epilogue saves 0.7 k,
 // its GEMM loses 1.3 k (bias loads ahead of the first MFMA).
-template <int MR, int NR, int ACT>
+template <int MR, int NR, int ACT, bool HOUT = false>
 __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], int wave, int lane,
                                               f32x16 (&acc)[MR][NR], unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
@@ -335,8 +365,13 @@ __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], i
         for (int k = 0; k < 4; ++k) {
           const int q = q0 + 2 * k;
           const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;  // row of q + 1 is row + 1
-          H[row * kLd + col] = t[k].x;
-          H[(row + 1) * kLd + col] = t[k].y;
+          if constexpr (HOUT) {
+            store_h1(H, row, col, t[k].x);
+            store_h1(H, row + 1, col, t[k].y);
+          } else {
+            H[row * kLd + col] = t[k].x;
+            H[(row + 1) * kLd + col] = t[k].y;
+          }
         }
       }
   }
@@ -349,7 +384,7 @@ __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], i
 // time, phase by phase, so the dependent exp / rcp chains of different
 // elements overlap (one element pair at a time, each step waiting on the last,
 // cost ~100 cycles per pair).  bf16x6 / fp16x3: 2-3 % faster than the C layout.
-template <int MR, int NR, int ACT>
+template <int MR, int NR, int ACT, bool HOUT = false>
 __device__ __forceinline__ void layer_store(float *H, int wave, int lane, f32x16 (&acc)[MR][NR],
                                             unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
@@ -367,8 +402,13 @@ __device__ __forceinline__ void layer_store(float *H, int wave, int lane, f32x16
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[k] = f32x2{acc[m][j][q0 + 2 * k], acc[m][j][q0 + 2 * k + 1]};
         act_apply2x4<ACT>(t);
-        *reinterpret_cast<f32x4 *>(row + 2 * q0) = f32x4{t[0].x, t[0].y, t[1].x, t[1].y};
-        *reinterpret_cast<f32x4 *>(row + 2 * q0 + 8) = f32x4{t[2].x, t[2].y, t[3].x, t[3].y};
+        if constexpr (HOUT) {
+          store_h4(H, m * 32 + r, col0 + 2 * q0, f32x4{t[0].x, t[0].y, t[1].x, t[1].y});
+          store_h4(H, m * 32 + r, col0 + 2 * q0 + 8, f32x4{t[2].x, t[2].y, t[3].x, t[3].y});
+        } else {
+          *reinterpret_cast<f32x4 *>(row + 2 * q0) = f32x4{t[0].x, t[0].y, t[1].x, t[1].y};
+          *reinterpret_cast<f32x4 *>(row + 2 * q0 + 8) = f32x4{t[2].x, t[2].y, t[3].x, t[3].y};
+        }
       }
     }
   }
@@ -543,27 +583,11 @@ __device__ __forceinline__ void static_for(F &&f) {
 // range ends at 65504.  Accuracy on the reference architecture: max |d| to a
 // float64 forward 3.6e-7, the same as numpy's float32 forward (test_gpu_parity).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 struct Split2 {
   f16x8 hi, lo;
 };
 
-__device__ __forceinline__ Split2 split2h(f32x8 x) {
-  Split2 s;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const f32x2 v = {x[2 * i], x[2 * i + 1]};
-    const f16x2 h = __builtin_convertvector(v, f16x2);
-    const f32x2 r = v - __builtin_convertvector(h, f32x2);
-    const f16x2 l = __builtin_convertvector(r, f16x2);
-    s.hi[2 * i] = h[0];
-    s.hi[2 * i + 1] = h[1];
-    s.lo[2 * i] = l[0];
-    s.lo[2 * i + 1] = l[1];
-  }
-  return s;
-}
 
 // weight planes of one K step: plane p (0 hi, 1 lo) of step g of column tile
 // nt is block (nt * G16 + g) * 2 + p of 64 lanes x 16 B
@@ -590,17 +614,26 @@ __device__ __forceinline__ void load_wh(WStepH<NR> &w, const WStream<NR> &ws, in
 // for 3 at 1M points (tools/ann_ab.sh): the weight stream is not latency-bound
 // but at the L2's rate for a table every CU reads (DESIGN.md "fp16x3").
 constexpr int kXRing = IKHIP_ANN_XRING;
+// A fragments of K step g from the split planes (store_h4 / store_h1): lane: row
+// lane & 31, k 16g + 8 (lane >> 5) + 0..7, one ds_read_b128 per plane.
+template <int MR>
+__device__ __forceinline__ void load_ah(Split2 (&a)[MR], const _Float16 *ap, int g) {
+#pragma unroll
+  for (int m = 0; m < MR; ++m) {
+    const _Float16 *q = ap + m * 32 * 2 * kLd + 16 * g;
+    a[m].hi = *reinterpret_cast<const f16x8 *>(q);
+    a[m].lo = *reinterpret_cast<const f16x8 *>(q + 512);
+  }
+}
+
 template <int MR, int NR, int GI>
 __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WStepH<NR> &fill,
-                                       const WStream<NR> &ws, const float *ab, int g,
+                                       const WStream<NR> &ws, const _Float16 *ab, int g,
                                        f32x16 (&acc)[MR][NR]) {
   __builtin_amdgcn_sched_barrier(0);
   load_wh(fill, ws, g + kXRing - 1);
-  f32x8 an[MR];
-  load_a(an, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
   Split2 sn[MR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m) sn[m] = split2h(an[m]);
+  load_ah(sn, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
 #pragma unroll
   for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -630,28 +663,23 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
                                              int G16, int xbytes, float xinv, int wave, int lane,
                                              const float *bias, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
-  const float *ap = H + r * kLd + 8 * h;
+  const _Float16 *ap = hplane(const_cast<float *>(H), r) + 8 * h;  // the split planes
   acc_init_bias(acc, bias, wave, kWaves, lane, 1.0f / xinv);  // exact: xinv is 2^-k
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 2, lane);
   WStepH<NR> w[kXRing];
 #pragma unroll
   for (int u = 0; u < kXRing - 1; ++u) load_wh(w[u], ws, u);
   Split2 sa[MR];
-  {
-    f32x8 a0[MR];
-    load_a(a0, ap, 0);
-#pragma unroll
-    for (int m = 0; m < MR; ++m) sa[m] = split2h(a0[m]);
-  }
+  load_ah(sa, ap, 0);
   int g = 0;
   for (; g + kXRing <= G16; g += kXRing) {
-    const float *ab = ap + 16 * g;
+    const _Float16 *ab = ap + 16 * g;
     static_for<kXRing>([&](auto u) {
       step_h<MR, NR, u.value>(sa, w[u.value], w[(u.value + kXRing - 1) % kXRing], ws, ab,
                               g + u.value, acc);
     });
   }
-  const float *ab = ap + 16 * g;
+  const _Float16 *ab = ap + 16 * g;
   static_for<kXRing - 1>([&](auto u) {
     if (g + u.value < G16)
       step_h<MR, NR, u.value>(sa, w[u.value], w[(u.value + kXRing - 1) % kXRing], ws, ab,
@@ -665,40 +693,52 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
 
 // One Dense layer for a wave with NR column tiles.  X: 0 fp32, 1 bf16x6,
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
-// a layer that stays fp32.
-template <int MR, int NR, int X = 0>
+// a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
+// layer is one) stores the activations as split planes.
+template <int ACT, bool HOUT, int MR, int NR>
+__device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[NR], int wave,
+                                          int lane, f32x16 (&acc)[MR][NR],
+                                          unsigned long long *st) {
+  if (tr) layer_store<MR, NR, ACT, HOUT>(H, wave, lane, acc, st);
+  else layer_store_c<MR, NR, ACT, HOUT>(H, bv, wave, lane, acc, st);
+}
+
+template <bool HOUT, int MR, int NR>
+__device__ __forceinline__ void store_act(int act, bool tr, float *H, const float (&bv)[NR],
+                                          int wave, int lane, f32x16 (&acc)[MR][NR],
+                                          unsigned long long *st) {
+  switch (act) {
+    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT>(tr, H, bv, wave, lane, acc, st); break;
+    default: store_any<IK_ACT_LINEAR, HOUT>(tr, H, bv, wave, lane, acc, st); break;
+  }
+}
+
+template <int MR, int NR, int X = 0, bool HX = false>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           unsigned long long *st_first,
                                           const void *wx = nullptr, int G16 = 0,
-                                          float xinv = 1.0f) {
+                                          float xinv = 1.0f, bool hout = false) {
   f32x16 acc[MR][NR];
   const int NT = wbytes / (G * 1024);  // column tiles of the layer
-  if (X != 0 && wx) {
+  float bv[NR];
+  const bool tr = X != 0 && wx;  // split GEMM: transposed tile, bias in the accumulators
+  if (tr) {
     if (X == 1)
       layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024, wave,
                            lane, bias, acc);
     else
       layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024, xinv,
                            wave, lane, bias, acc);
-    switch (act) {
-      case IK_ACT_TANH: layer_store<MR, NR, IK_ACT_TANH>(H, wave, lane, acc, st); break;
-      case IK_ACT_RELU: layer_store<MR, NR, IK_ACT_RELU>(H, wave, lane, acc, st); break;
-      case IK_ACT_SIGMOID: layer_store<MR, NR, IK_ACT_SIGMOID>(H, wave, lane, acc, st); break;
-      default: layer_store<MR, NR, IK_ACT_LINEAR>(H, wave, lane, acc, st); break;
-    }
-    return;
-  }
-  float bv[NR];
+  } else {
 #pragma unroll
-  for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + kWaves * j) * 32 + (lane & 31)];
-  layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, nullptr, acc, st_first);
-  switch (act) {
-    case IK_ACT_TANH: layer_store_c<MR, NR, IK_ACT_TANH>(H, bv, wave, lane, acc, st); break;
-    case IK_ACT_RELU: layer_store_c<MR, NR, IK_ACT_RELU>(H, bv, wave, lane, acc, st); break;
-    case IK_ACT_SIGMOID: layer_store_c<MR, NR, IK_ACT_SIGMOID>(H, bv, wave, lane, acc, st); break;
-    default: layer_store_c<MR, NR, IK_ACT_LINEAR>(H, bv, wave, lane, acc, st); break;
+    for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + kWaves * j) * 32 + (lane & 31)];
+    layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, nullptr, acc, st_first);
   }
+  if (HX && hout) store_act<true>(act, tr, H, bv, wave, lane, acc, st);
+  else store_act<false>(act, tr, H, bv, wave, lane, acc, st);
 }
 
 template <int BM, int ACT>
@@ -794,6 +834,9 @@ __global__ __launch_bounds__(256, (MR == 2 || kWide) ? 1 : 2) void ann_fused_ker
       unsigned long long *sl = (stp && l < 14) ? stp + 2 + 2 * l : nullptr;
       unsigned long long *sf = (stp && l == 5) ? stp + 30 : nullptr;  // layer 5's first group
       const void *wx = X ? a.m.wx[l] : nullptr;
+      // fp16x3: the next layer reads split planes when it runs the split GEMM
+      const bool hout = X == 2 && l + 1 < a.m.n_layers && a.m.wx[l + 1] &&
+                        (a.m.np[l + 1] >> 5) > 1;
       if (NT == 1) {
         run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid, sl);
       } else if (X && wx) {
@@ -801,19 +844,19 @@ __global__ __launch_bounds__(256, (MR == 2 || kWide) ? 1 : 2) void ann_fused_ker
         const int G16 = (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
-          case 3: run_layer<MR, 3, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
-          case 2: run_layer<MR, 2, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
-          case 1: run_layer<MR, 1, X>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv); break;
+          case 4: run_layer<MR, 4, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 3: run_layer<MR, 3, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 2: run_layer<MR, 2, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 1: run_layer<MR, 1, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
           default: __syncthreads(); break;
         }
       } else {
         const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
-          case 3: run_layer<MR, 3>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
-          case 2: run_layer<MR, 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
-          case 1: run_layer<MR, 1>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 4: run_layer<MR, 4, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 3: run_layer<MR, 3, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 2: run_layer<MR, 2, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 1: run_layer<MR, 1, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
 #ifdef IKHIP_ANN_WIDE
           case 8: run_layer<MR, 8>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
           case 7: run_layer<MR, 7>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;

@@ -1,13 +1,24 @@
-# Build inversekinematicsann_amd/libikhip_prev.so: the library with ik_fabrik.hip
-# (or the file given) from git HEAD, for same-box A/B runs (tools/fab_ab.sh).
+# Build inversekinematicsann_amd/libikhip_prev.so: the library with the csrc/
+# sources of git HEAD, for same-box A/B runs against the working tree
+# (tools/fab_ab.sh, tools/ann_ab.sh).
 set -e
-cd "$(dirname "$0")/../inversekinematicsann_amd/csrc"
-F=${1:-ik_fabrik}
-git show HEAD:inversekinematicsann_amd/csrc/$F.hip > ${F}_prev.hip
-trap 'rm -f ${F}_prev.hip' EXIT
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -c ${F}_prev.hip -o /tmp/${F}_prev.o
-objs=""
-for o in ik_fk ik_fabrik ik_ann ik_ann_x ik_ann_w ik_shard ik_pipe ik_api; do
-  if [ "$o" = "$F" ]; then objs="$objs /tmp/${F}_prev.o"; else objs="$objs $o.o"; fi
+ROOT="$(cd "$(dirname "$0")/.." && pwd)"
+T=$(mktemp -d /tmp/ikprev.XXXXXX)
+trap 'rm -rf $T' EXIT
+mkdir -p $T/a/csrc $T/include
+git -C "$ROOT" show HEAD:include/ikhip.h > $T/include/ikhip.h
+for f in $(git -C "$ROOT" ls-tree --name-only HEAD inversekinematicsann_amd/csrc/); do
+  git -C "$ROOT" show HEAD:$f > $T/a/csrc/$(basename $f)
 done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../libikhip_prev.so $objs
+cd $T/a/csrc
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off"
+objs=""
+for o in ik_fk ik_fabrik ik_ann ik_ann_x ik_ann_w ik_shard; do
+  /opt/rocm/bin/hipcc $FLAGS -c $o.hip -o $o.o & objs="$objs $o.o"
+done
+for o in ik_pipe ik_api; do
+  /opt/rocm/bin/hipcc $FLAGS -x hip -c $o.cpp -o $o.o & objs="$objs $o.o"
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/inversekinematicsann_amd/libikhip_prev.so" $objs
+echo "built libikhip_prev.so from HEAD"
