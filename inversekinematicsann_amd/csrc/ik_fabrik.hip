@@ -464,10 +464,14 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
 // into shard b % kOrdShards, claims its run inside its region with one atomic
 // per class and hands the slots out through LDS atomics.
 __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
+  static_assert(kOrdClasses * kOrdShards == 256, "one total per thread");
   __shared__ unsigned int cnt[kOrdClasses], base[kOrdClasses];
+  __shared__ unsigned int tot[kOrdClasses][kOrdShards], ctot[kOrdClasses];
   const int t = threadIdx.x;
   const int sh = blockIdx.x % kOrdShards;
   if (t < kOrdClasses) cnt[t] = 0;
+  // the 256 (class, shard) totals, one load per thread, in flight with the cells
+  tot[t / kOrdShards][t % kOrdShards] = (&a.S->cls_tot[0][0])[t];
   const int64_t b0 = (int64_t)blockIdx.x * (256 * kOrdPPT);
   uint16_t cl[kOrdPPT];
 #pragma unroll
@@ -479,12 +483,18 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
 #pragma unroll
   for (int j = 0; j < kOrdPPT; ++j)
     if (cl[j] != 0xffff) atomicAdd(&cnt[cl[j] >> 10], 1u);
+  if (t < kOrdClasses) {
+    unsigned int c = 0;
+#pragma unroll
+    for (int q = 0; q < kOrdShards; ++q) c += tot[t][q];
+    ctot[t] = c;
+  }
   __syncthreads();
   if (t < kOrdClasses) {
+    // region (t, sh) starts after every harder class and the lower shards of t
     unsigned int start = 0;
-    for (int c = kOrdClasses - 1; c > t; --c)
-      for (int q = 0; q < kOrdShards; ++q) start += a.S->cls_tot[c][q];
-    for (int q = 0; q < sh; ++q) start += a.S->cls_tot[t][q];
+    for (int c = kOrdClasses - 1; c > t; --c) start += ctot[c];
+    for (int q = 0; q < sh; ++q) start += tot[t][q];
     base[t] = start + (cnt[t] ? atomicAdd(&a.S->cls_cur[t][sh], cnt[t]) : 0u);
   }
   __syncthreads();
