@@ -448,10 +448,15 @@ def end_to_end(job, solve_host, args):
     import torch
     from inversekinematicsann_amd import _native
     pts = job.pts if job.sc is not None else job.pts[job.lo:job.hi]
-    reps = max(1, min(args.steps, 3))
+    reps = max(1, min(args.steps, 10))
 
     def rate(host_pts, pinned):
-        solve_host(host_pts, pinned)  # warm the staging scratch
+        # untimed warm-up: the staging scratch, the pipeline's streams, and the
+        # copy engines' queues, which the runtime sets up over the first calls (the
+        # first pinned calls of a process measured 19-22 / 7.7-10 / 1.2-8.3 ms,
+        # steady 1.10-1.13: tools/pinned_probe.py)
+        for _ in range(5):
+            solve_host(host_pts, pinned)
         barrier(job.world)
         t0 = time.perf_counter()
         for _ in range(reps):

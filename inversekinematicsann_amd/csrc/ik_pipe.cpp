@@ -41,9 +41,19 @@ int64_t pipe_min_points() {
   return v;
 }
 
+int64_t pipe_chunk_points() {
+  static int64_t v = -1;
+  if (v < 0) {
+    const char *e = std::getenv("IKHIP_PIPE_CHUNK");  // points per chunk
+    v = (e && *e && std::atoll(e) > 0) ? std::atoll(e) : 262144;
+  }
+  return v;
+}
+
 int chunks_for(int64_t n) {
   // ~250k points per chunk (1M points: 4), 2..8 chunks
-  int64_t k = (n + 262143) / 262144;
+  const int64_t c = pipe_chunk_points();
+  int64_t k = (n + c - 1) / c;
   return (int)(k < 2 ? 2 : (k > kPipeMaxChunks ? kPipeMaxChunks : k));
 }
 
@@ -152,10 +162,11 @@ static int run_chunks(ik_ctx *c, int K, const int64_t *begin, const double *pts,
     IK_HIP(hipStreamWaitEvent(c->stream, p.ev_in[k], 0));
     int rc = launch(k, b, m);
     if (rc) return rc;
-    IK_HIP(hipMemcpyAsync(&p.h_stats[k], &p.d_stats[k], sizeof(DevStats), hipMemcpyDeviceToHost,
-                          c->stream));
     IK_HIP(hipEventRecord(p.ev_done[k], c->stream));
     IK_HIP(hipStreamWaitEvent(p.s_out, p.ev_done[k], 0));
+    // every D2H on the copy-out stream (the compute stream issues no copies)
+    IK_HIP(hipMemcpyAsync(&p.h_stats[k], &p.d_stats[k], sizeof(DevStats), hipMemcpyDeviceToHost,
+                          p.s_out));
     for (int r = 0; r < nout; ++r)
       if (outs[r].host)
         IK_HIP(hipMemcpyAsync(outs[r].host + b * outs[r].row, outs[r].dev + b * outs[r].row,

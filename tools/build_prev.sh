@@ -6,9 +6,11 @@ ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 T=$(mktemp -d /tmp/ikprev.XXXXXX)
 trap 'rm -rf $T' EXIT
 mkdir -p $T/a/csrc $T/include
-git -C "$ROOT" show HEAD:include/ikhip.h > $T/include/ikhip.h
-for f in $(git -C "$ROOT" ls-tree --name-only HEAD inversekinematicsann_amd/csrc/); do
-  git -C "$ROOT" show HEAD:$f > $T/a/csrc/$(basename $f)
+REV=${REV:-HEAD}
+OUT=${OUT:-libikhip_prev.so}
+git -C "$ROOT" show $REV:include/ikhip.h > $T/include/ikhip.h
+for f in $(git -C "$ROOT" ls-tree --name-only $REV inversekinematicsann_amd/csrc/); do
+  git -C "$ROOT" show $REV:$f > $T/a/csrc/$(basename $f)
 done
 cd $T/a/csrc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off"
@@ -20,5 +22,5 @@ for o in ik_pipe ik_api; do
   /opt/rocm/bin/hipcc $FLAGS -x hip -c $o.cpp -o $o.o & objs="$objs $o.o"
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/inversekinematicsann_amd/libikhip_prev.so" $objs
-echo "built libikhip_prev.so from HEAD"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/inversekinematicsann_amd/$OUT" $objs
+echo "built $OUT from $REV"
