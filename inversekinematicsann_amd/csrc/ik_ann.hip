@@ -741,13 +741,18 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   else store_act<false>(act, tr, H, bv, wave, lane, acc, st);
 }
 
-template <int BM, int ACT>
+// HOUT: the next layer runs fp16x3, so the result goes out as split planes
+// (bytes [0, 64) and [1024, 1088) of the row: clear of the partials at floats
+// 32..159, which other threads of the block are still reading).
+template <int BM, int ACT, bool HOUT = false>
 __device__ __forceinline__ void splitk_finish(float *H, const float *__restrict__ bias, int tid) {
   for (int o = tid; o < BM * 32; o += kWaves * 64) {
     const int row = o >> 5, col = o & 31;
     const float *p = H + row * kLd + 32 + col;
     float v = ((p[0] + p[32]) + p[64]) + p[96];  // fixed order: deterministic
-    H[row * kLd + col] = act_apply<ACT>(v + bias[col]);
+    const float y = act_apply<ACT>(v + bias[col]);
+    if constexpr (HOUT) store_h1(H, row, col, y);
+    else H[row * kLd + col] = y;
   }
 }
 
@@ -755,10 +760,10 @@ __device__ __forceinline__ void splitk_finish(float *H, const float *__restrict_
 // ann.py:56): the K range is split over the 4 waves, the partial BM x 32 tiles
 // go to LDS columns 32..159 (never read by this or the next layer) and are
 // summed in a fixed order, so no wave idles.
-template <int MR>
+template <int MR, bool HX = false>
 __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, const float *bias,
                                                  int act, int G, int wave, int lane, int tid,
-                                                 unsigned long long *st) {
+                                                 unsigned long long *st, bool hout = false) {
   constexpr int BM = 32 * MR;
   f32x16 acc[MR][1];
   const int g0 = (G * wave) / kWaves, g1 = (G * (wave + 1)) / kWaves;
@@ -775,10 +780,22 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
     }
   __syncthreads();
   switch (act) {
-    case IK_ACT_TANH: splitk_finish<BM, IK_ACT_TANH>(H, bias, tid); break;
-    case IK_ACT_RELU: splitk_finish<BM, IK_ACT_RELU>(H, bias, tid); break;
-    case IK_ACT_SIGMOID: splitk_finish<BM, IK_ACT_SIGMOID>(H, bias, tid); break;
-    default: splitk_finish<BM, IK_ACT_LINEAR>(H, bias, tid); break;
+    case IK_ACT_TANH:
+      if (HX && hout) splitk_finish<BM, IK_ACT_TANH, true>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_TANH>(H, bias, tid);
+      break;
+    case IK_ACT_RELU:
+      if (HX && hout) splitk_finish<BM, IK_ACT_RELU, true>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_RELU>(H, bias, tid);
+      break;
+    case IK_ACT_SIGMOID:
+      if (HX && hout) splitk_finish<BM, IK_ACT_SIGMOID, true>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_SIGMOID>(H, bias, tid);
+      break;
+    default:
+      if (HX && hout) splitk_finish<BM, IK_ACT_LINEAR, true>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_LINEAR>(H, bias, tid);
+      break;
   }
 }
 
@@ -838,7 +855,7 @@ __global__ __launch_bounds__(256, (MR == 2 || kWide) ? 1 : 2) void ann_fused_ker
       const bool hout = X == 2 && l + 1 < a.m.n_layers && a.m.wx[l + 1] &&
                         (a.m.np[l + 1] >> 5) > 1;
       if (NT == 1) {
-        run_layer_splitk<MR>(H, wp, bias, act, G, wave, lane, tid, sl);
+        run_layer_splitk<MR, X == 2>(H, wp, bias, act, G, wave, lane, tid, sl, hout);
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
         const int G16 = (a.m.kp[l] + 15) >> 4;

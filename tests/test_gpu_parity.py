@@ -270,6 +270,7 @@ def test_ann_width_cap(ctx1):
     ((3, 100, 37, 250, 4), "tanh"),             # ragged: K not a multiple of 16, NR 1..4
     ((3, 512, 512, 4), "relu"),                 # fp16x3: unbounded input -> fp32 layer
     ((3, 96, 96, 4), "sigmoid"),
+    ((3, 64, 32, 64, 4), "tanh"),               # a split-K (32-wide) layer feeds a split one
 ])
 def test_ann_split_modes(ctx1, dims, act, mode):
     """IK_ANN_BF16X6 / IK_ANN_FP16X3: split hidden GEMMs stay within the
@@ -287,6 +288,36 @@ def test_ann_split_modes(ctx1, dims, act, mode):
     d_f = np.abs(ang_f.astype(np.float64) - ref64).max()
     print(f"{mode} {dims[:3]}.. {act}: max|d| {d_x:.3e} (fp32 mode {d_f:.3e})")
     assert d_x <= NS_TOL, d_x             # north_star: 1e-5 absolute
+    assert d_x <= 4 * d_f + 2e-7, (d_x, d_f)
+
+
+def test_ann_fp16x3_layer_mix(ctx1):
+    """fp16x3 on a model whose layers switch between the split GEMM (input bounded:
+    after tanh / sigmoid) and fp32 (after relu / linear, or 32-wide split-K layers),
+    so the activations go out as split fp16 planes exactly where the next layer reads
+    them that way: within 1e-5 of a float64 forward and of the fp32 mode's distance."""
+    from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER as XS, \
+        REFERENCE_Y_SCALER as YS
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    dims = (3, 200, 160, 32, 96, 128, 64, 4)
+    m = glorot_model(dims=dims, seed=31)
+    m.activations[:] = ["tanh", "relu", "tanh", "sigmoid", "linear", "tanh", "linear"]
+    rng = np.random.default_rng(31)
+    for b in m.biases:
+        b[:] = rng.normal(0, 0.1, b.shape).astype(np.float32)
+    pts = random_dist(3001, seed=31)
+    ref64 = O.ann_forward(pts, m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean,
+                          YS.scale, compute=np.float64)
+    ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    try:
+        ctx1.ann_set_mode("fp16x3")
+        ang_x, _, _ = ctx1.ann_solve(pts, check_limits=False)
+    finally:
+        ctx1.ann_set_mode("fp32")
+    ang_f, _, _ = ctx1.ann_solve(pts, check_limits=False)
+    d_x = np.abs(ang_x.astype(np.float64) - ref64).max()
+    d_f = np.abs(ang_f.astype(np.float64) - ref64).max()
+    assert d_x <= NS_TOL, d_x
     assert d_x <= 4 * d_f + 2e-7, (d_x, d_f)
 
 
