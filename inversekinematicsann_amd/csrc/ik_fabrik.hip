@@ -591,9 +591,14 @@ fabrik_iter_kernel(FabArgs a) {
   asm volatile("" : "+v"(tol2), "+v"(max_iter));
   double L[4] = {a.r.links[0], a.r.links[1], a.r.links[2], a.r.links[3]};
 
-  // prepared points: lane j holds the batch's entry j (wave-uniform count / cursor)
-  d3 P0 = {0, 0, 0}, P1 = P0, P2 = P0, Pg = P0;
-  int64_t Pidx = 0;
+  // prepared points: the batch's entry j in slot j of the wave's LDS batch
+  // (wave-uniform count / cursor); a refilled lane reads its entry from there
+  struct PrepBatch {
+    double v[12][64];  // seed joints 0..2 and the goal
+    long long idx[64];
+  };
+  __shared__ PrepBatch batches[4];
+  PrepBatch &PB = batches[threadIdx.x >> 6];
   int pcount = 0, pptr = 0;
   // the next batch, fetched in stages while the current one is handed out (so
   // that no stage waits for memory): 0 none, 1 queue grab issued (na), 2 its
@@ -744,15 +749,15 @@ fabrik_iter_kernel(FabArgs a) {
 #else
             Js[0] = {0.0, 0.0, 2.0}; Js[1] = {ng.x * 0.1, ng.y * 0.1, 4.0}; Js[2] = {ng.x * 0.2, ng.y * 0.2, 6.0};
 #endif
-            P0 = Js[0];
-            P1 = Js[1];
-            P2 = Js[2];
-            Pg = ng;
-            Pidx = ni;
+            PB.v[0][lane] = Js[0].x; PB.v[1][lane] = Js[0].y; PB.v[2][lane] = Js[0].z;
+            PB.v[3][lane] = Js[1].x; PB.v[4][lane] = Js[1].y; PB.v[5][lane] = Js[1].z;
+            PB.v[6][lane] = Js[2].x; PB.v[7][lane] = Js[2].y; PB.v[8][lane] = Js[2].z;
+            PB.v[9][lane] = ng.x; PB.v[10][lane] = ng.y; PB.v[11][lane] = ng.z;
+            PB.idx[lane] = ni;
           }
 #ifdef IKHIP_DIAG
           // (the seed's loads are consumed before the stamp)
-          asm volatile("" ::"v"(P0.x), "v"(P1.x), "v"(P2.x), "v"(Pg.x));
+          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the batch's LDS writes landed
 #endif
           IKHIP_DT_ACC(kDiagPrepTicks, kDiagTDrain);
           IKHIP_DT_ACC(kDiagTRefill, kDiagTDrain);  // (not refill time)
@@ -760,15 +765,13 @@ fabrik_iter_kernel(FabArgs a) {
         const int take = min(nfree - handed, pcount - pptr);
         const bool mine = wasfree && rank >= handed && rank < handed + take;
         const int src = mine ? pptr + (rank - handed) : lane;
-        const d3 n0 = shfl3(P0, src), n1 = shfl3(P1, src), n2 = shfl3(P2, src);
-        const d3 gq = shfl3(Pg, src);
-        const int64_t iq = __shfl(Pidx, src, 64);
+        __builtin_amdgcn_wave_barrier();  // the batch's LDS writes before the reads
         if (mine) {
-          J0 = n0;
-          J1 = n1;
-          J2 = n2;
-          g = gq;
-          out = iq;
+          J0 = {PB.v[0][src], PB.v[1][src], PB.v[2][src]};
+          J1 = {PB.v[3][src], PB.v[4][src], PB.v[5][src]};
+          J2 = {PB.v[6][src], PB.v[7][src], PB.v[8][src]};
+          g = {PB.v[9][src], PB.v[10][src], PB.v[11][src]};
+          out = PB.idx[src];
           st = IK_OK;
           se = 1.0;
           ge = 1.0;
