@@ -287,11 +287,7 @@ __device__ __forceinline__ bool outside_rc(RcConst k, d3 g) {
 __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const d3 J[4], d3 g,
                                              int it, int st, LaneAcc &acc) {
   double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
-#ifndef IKHIP_EXP_NOANGLES
   if (st == IK_OK) get_angles(J, th, st);
-#else
-  th[0] = J[3].x; th[1] = J[3].y; th[2] = J[3].z; th[3] = J[2].x;
-#endif
   if (st != IK_OK) record_error(a.S, i, st);
   double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
   o[0] = make_double2(th[0], th[1]);
@@ -301,7 +297,6 @@ __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const 
   acc.sum_it += (unsigned long long)it;
   acc.capped += (it >= a.max_iter) ? 1ull : 0ull;
   acc.max_it = max(acc.max_it, it);
-#ifndef IKHIP_EXP_NOFK
   if (a.fk_err) {
     double e = __builtin_nan("");
     if (st == IK_OK) {
@@ -317,7 +312,6 @@ __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const 
       acc.fk_sum += e;
     }
   }
-#endif
 }
 
 // ------------------------------------------------------------- simple ----
@@ -563,9 +557,6 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ d3 shfl3(const d3 v, int src) {
-  return {__shfl(v.x, src, 64), __shfl(v.y, src, 64), __shfl(v.z, src, 64)};
-}
 
 // ORD: the queue is a.perm (work order above), else point order.  CORE: 0
 // general sqrt / division, 1 sqrt_core / div_core, 2 the same with the repeated
@@ -744,11 +735,7 @@ fabrik_iter_kernel(FabArgs a) {
             if (a.check_limits && outside_rc(k, ng))
               atomicMin(&a.S->first_oob, (unsigned long long)ni);
             d3 Js[4];
-#ifndef IKHIP_EXP_NOSEED
             (void)seed_pose((const RobotConstDev *)k, ng, Js);
-#else
-            Js[0] = {0.0, 0.0, 2.0}; Js[1] = {ng.x * 0.1, ng.y * 0.1, 4.0}; Js[2] = {ng.x * 0.2, ng.y * 0.2, 6.0};
-#endif
             PB.v[0][lane] = Js[0].x; PB.v[1][lane] = Js[0].y; PB.v[2][lane] = Js[0].z;
             PB.v[3][lane] = Js[1].x; PB.v[4][lane] = Js[1].y; PB.v[5][lane] = Js[1].z;
             PB.v[6][lane] = Js[2].x; PB.v[7][lane] = Js[2].y; PB.v[8][lane] = Js[2].z;
