@@ -343,7 +343,7 @@ __device__ __forceinline__ void store_h1(float *H, int row, int col, float v) {
 // transposed form below (bias in the accumulators, b128 stores) measured
 // 0.6 k cycles per layer slower here: its 5.9 k-cycle epilogue saves 0.7 k,
 // its GEMM loses 1.3 k (bias loads ahead of the first MFMA).
-template <int MR, int NR, int ACT, bool HOUT = false>
+template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
 __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], int wave, int lane,
                                               f32x16 (&acc)[MR][NR], unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
@@ -351,7 +351,7 @@ __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], i
   __syncthreads();  // every wave has finished reading the layer input
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
-    const int col = (wave + kWaves * j) * 32 + r;
+    const int col = (wave + W * j) * 32 + r;
 #pragma unroll
     for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -384,7 +384,7 @@ __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], i
 // time, phase by phase, so the dependent exp / rcp chains of different
 // elements overlap (one element pair at a time, each step waiting on the last,
 // cost ~100 cycles per pair).  bf16x6 / fp16x3: 2-3 % faster than the C layout.
-template <int MR, int NR, int ACT, bool HOUT = false>
+template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
 __device__ __forceinline__ void layer_store(float *H, int wave, int lane, f32x16 (&acc)[MR][NR],
                                             unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
@@ -392,7 +392,7 @@ __device__ __forceinline__ void layer_store(float *H, int wave, int lane, f32x16
   __syncthreads();  // every wave has finished reading the layer input
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
-    const int col0 = (wave + kWaves * j) * 32 + 4 * h;
+    const int col0 = (wave + W * j) * 32 + 4 * h;
 #pragma unroll
     for (int m = 0; m < MR; ++m) {
       float *row = H + (m * 32 + r) * kLd + col0;
@@ -529,14 +529,14 @@ __device__ __forceinline__ void step_x(Split3 (&sa)[MR], const WStep<NR> &w, WSt
 
 // Full-width layer in bf16x6 mode (NR column tiles per wave).  A reads of the
 // step after the last run into the next row or H's pad, never multiplied.
-template <int MR, int NR>
+template <int MR, int NR, int W = kWaves>
 __device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__restrict__ wx,
                                              int G16, int xbytes, int wave, int lane,
                                              const float *bias, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 8 * h;
-  acc_init_bias(acc, bias, wave, kWaves, lane);
-  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 3, lane);
+  acc_init_bias(acc, bias, wave, W, lane);
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G16 * 3, lane);
   WStep<NR> w0, w1, w2;
   load_w(w0, ws, 0);
   load_w(w1, ws, 1);
@@ -658,14 +658,14 @@ __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WS
 }
 
 // Full-width layer in fp16x3 mode; the accumulators come back scaled by xinv.
-template <int MR, int NR>
+template <int MR, int NR, int W = kWaves>
 __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__restrict__ wx,
                                              int G16, int xbytes, float xinv, int wave, int lane,
                                              const float *bias, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
   const _Float16 *ap = hplane(const_cast<float *>(H), r) + 8 * h;  // the split planes
-  acc_init_bias(acc, bias, wave, kWaves, lane, 1.0f / xinv);  // exact: xinv is 2^-k
-  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, kWaves, G16 * 2, lane);
+  acc_init_bias(acc, bias, wave, W, lane, 1.0f / xinv);  // exact: xinv is 2^-k
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G16 * 2, lane);
   WStepH<NR> w[kXRing];
 #pragma unroll
   for (int u = 0; u < kXRing - 1; ++u) load_wh(w[u], ws, u);
@@ -695,27 +695,27 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
 // a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
 // layer is one) stores the activations as split planes.
-template <int ACT, bool HOUT, int MR, int NR>
+template <int ACT, bool HOUT, int W, int MR, int NR>
 __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[NR], int wave,
                                           int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st) {
-  if (tr) layer_store<MR, NR, ACT, HOUT>(H, wave, lane, acc, st);
-  else layer_store_c<MR, NR, ACT, HOUT>(H, bv, wave, lane, acc, st);
+  if (tr) layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
+  else layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
 }
 
-template <bool HOUT, int MR, int NR>
+template <bool HOUT, int W, int MR, int NR>
 __device__ __forceinline__ void store_act(int act, bool tr, float *H, const float (&bv)[NR],
                                           int wave, int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st) {
   switch (act) {
-    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT>(tr, H, bv, wave, lane, acc, st); break;
-    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT>(tr, H, bv, wave, lane, acc, st); break;
-    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT>(tr, H, bv, wave, lane, acc, st); break;
-    default: store_any<IK_ACT_LINEAR, HOUT>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
+    default: store_any<IK_ACT_LINEAR, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
   }
 }
 
-template <int MR, int NR, int X = 0, bool HX = false>
+template <int MR, int NR, int X = 0, bool HX = false, int W = kWaves>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           unsigned long long *st_first,
@@ -727,26 +727,26 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   const bool tr = X != 0 && wx;  // split GEMM: transposed tile, bias in the accumulators
   if (tr) {
     if (X == 1)
-      layer_gemm_x<MR, NR>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024, wave,
-                           lane, bias, acc);
+      layer_gemm_x<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024,
+                              wave, lane, bias, acc);
     else
-      layer_gemm_h<MR, NR>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024, xinv,
-                           wave, lane, bias, acc);
+      layer_gemm_h<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024,
+                              xinv, wave, lane, bias, acc);
   } else {
 #pragma unroll
-    for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + kWaves * j) * 32 + (lane & 31)];
-    layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, kWaves, lane, nullptr, acc, st_first);
+    for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + W * j) * 32 + (lane & 31)];
+    layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, W, lane, nullptr, acc, st_first);
   }
-  if (HX && hout) store_act<true>(act, tr, H, bv, wave, lane, acc, st);
-  else store_act<false>(act, tr, H, bv, wave, lane, acc, st);
+  if (HX && hout) store_act<true, W>(act, tr, H, bv, wave, lane, acc, st);
+  else store_act<false, W>(act, tr, H, bv, wave, lane, acc, st);
 }
 
 // HOUT: the next layer runs fp16x3, so the result goes out as split planes
 // (bytes [0, 64) and [1024, 1088) of the row: clear of the partials at floats
 // 32..159, which other threads of the block are still reading).
-template <int BM, int ACT, bool HOUT = false>
+template <int BM, int ACT, bool HOUT = false, int W = kWaves>
 __device__ __forceinline__ void splitk_finish(float *H, const float *__restrict__ bias, int tid) {
-  for (int o = tid; o < BM * 32; o += kWaves * 64) {
+  for (int o = tid; o < BM * 32; o += W * 64) {
     const int row = o >> 5, col = o & 31;
     const float *p = H + row * kLd + 32 + col;
     float v = ((p[0] + p[32]) + p[64]) + p[96];  // fixed order: deterministic
@@ -760,17 +760,21 @@ __device__ __forceinline__ void splitk_finish(float *H, const float *__restrict_
 // ann.py:56): the K range is split over the 4 waves, the partial BM x 32 tiles
 // go to LDS columns 32..159 (never read by this or the next layer) and are
 // summed in a fixed order, so no wave idles.
-template <int MR, bool HX = false>
+template <int MR, bool HX = false, int W = kWaves>
 __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, const float *bias,
                                                  int act, int G, int wave, int lane, int tid,
                                                  unsigned long long *st, bool hout = false) {
   constexpr int BM = 32 * MR;
   f32x16 acc[MR][1];
-  const int g0 = (G * wave) / kWaves, g1 = (G * (wave + 1)) / kWaves;
+  // K split over the first four waves (their partials fill columns 32..159; any
+  // further waves only join the barriers)
+  const int ws = wave < 4 ? wave : 4;
+  const int g0 = (G * ws) / 4, g1 = wave < 4 ? (G * (wave + 1)) / 4 : g0;
   layer_gemm<MR, 1, false>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, nullptr, acc);
   stamp(st);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
+  if (wave < 4)
 #pragma unroll
   for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -781,20 +785,20 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
   __syncthreads();
   switch (act) {
     case IK_ACT_TANH:
-      if (HX && hout) splitk_finish<BM, IK_ACT_TANH, true>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_TANH>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_TANH, true, W>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_TANH, false, W>(H, bias, tid);
       break;
     case IK_ACT_RELU:
-      if (HX && hout) splitk_finish<BM, IK_ACT_RELU, true>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_RELU>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_RELU, true, W>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_RELU, false, W>(H, bias, tid);
       break;
     case IK_ACT_SIGMOID:
-      if (HX && hout) splitk_finish<BM, IK_ACT_SIGMOID, true>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_SIGMOID>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_SIGMOID, true, W>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_SIGMOID, false, W>(H, bias, tid);
       break;
     default:
-      if (HX && hout) splitk_finish<BM, IK_ACT_LINEAR, true>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_LINEAR>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_LINEAR, true, W>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_LINEAR, false, W>(H, bias, tid);
       break;
   }
 }
@@ -802,9 +806,23 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 // X: 0 fp32; 1 bf16x6, 2 fp16x3 -- layers whose split weight operand exists
 // (a.m.wx[l]) take the split GEMM; the others (input layer, split-K output
 // layer, fp16x3-ineligible layers) stay fp32.
+// Waves per workgroup: 4, one per SIMD (NR column tiles each, 4 at full width);
+// the fp16x3 kernel at 64-point tiles runs IKHIP_ANN_XWAVES (default 8: two per
+// SIMD, NR = 2), so that one wave's weight loads and LDS reads issue under the
+// other's MFMAs.
+#ifndef IKHIP_ANN_XWAVES
+#define IKHIP_ANN_XWAVES 8
+#endif
 template <int MR, int X>
-__global__ __launch_bounds__(256, (MR == 2 || kWide) ? 1 : 2) void ann_fused_kernel(AnnArgs a) {
+constexpr int ann_waves() {
+  return (X == 2 && MR == 2) ? IKHIP_ANN_XWAVES : kWaves;
+}
+
+template <int MR, int X>
+__global__ __launch_bounds__((64 * ann_waves<MR, X>()), (MR == 2 || kWide) ? 1 : 2) void
+ann_fused_kernel(AnnArgs a) {
   constexpr int BM = 32 * MR;
+  constexpr int W = ann_waves<MR, X>();
   // + kHPad: the fp32 GEMM's operand ring reads up to 3 K groups past a row's end
   __shared__ __attribute__((aligned(16))) float H[BM * kLd + kHPad];
   const int tid = threadIdx.x;
@@ -818,7 +836,7 @@ __global__ __launch_bounds__(256, (MR == 2 || kWide) ? 1 : 2) void ann_fused_ker
     // start, 1 staged, 2+2l layer l GEMM done, 3+2l layer l done, 31 tile done
     unsigned long long *stp = nullptr;
     const int64_t it_local = tile / gridDim.x;  // this workgroup's tile counter
-    if (a.dbg && blockIdx.x == 0 && lane == 0 && it_local < kStampTiles)
+    if (a.dbg && blockIdx.x == 0 && lane == 0 && it_local < kStampTiles && wave < kWaves)
       stp = a.dbg + ((size_t)it_local * kWaves + wave) * kStampSlots;
     stamp(stp);
     double px = 0.0, py = 0.0, pz = 0.0;
@@ -855,25 +873,33 @@ __global__ __launch_bounds__(256, (MR == 2 || kWide) ? 1 : 2) void ann_fused_ker
       const bool hout = X == 2 && l + 1 < a.m.n_layers && a.m.wx[l + 1] &&
                         (a.m.np[l + 1] >> 5) > 1;
       if (NT == 1) {
-        run_layer_splitk<MR, X == 2>(H, wp, bias, act, G, wave, lane, tid, sl, hout);
+        run_layer_splitk<MR, X == 2, W>(H, wp, bias, act, G, wave, lane, tid, sl, hout);
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
         const int G16 = (a.m.kp[l] + 15) >> 4;
-        const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
+        const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
-          case 3: run_layer<MR, 3, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
-          case 2: run_layer<MR, 2, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
-          case 1: run_layer<MR, 1, X, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 4:
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
+            break;
+          case 3:
+            if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
+            break;
+          case 2: run_layer<MR, 2, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 1: run_layer<MR, 1, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
           default: __syncthreads(); break;
         }
       } else {
-        const int cnt = (wave < NT) ? (NT - wave + kWaves - 1) / kWaves : 0;
+        const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
-          case 4: run_layer<MR, 4, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
-          case 3: run_layer<MR, 3, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
-          case 2: run_layer<MR, 2, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
-          case 1: run_layer<MR, 1, 0, X == 2>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 4:
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
+            break;
+          case 3:
+            if constexpr (W * 3 <= 16) run_layer<MR, 3, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
+            break;
+          case 2: run_layer<MR, 2, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 1: run_layer<MR, 1, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
 #ifdef IKHIP_ANN_WIDE
           case 8: run_layer<MR, 8>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
           case 7: run_layer<MR, 7>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
@@ -1146,7 +1172,8 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
 
 void ann::launch_ann_kernel_x(int mr, int xmode, unsigned grid, hipStream_t st,
                               const AnnArgs &a) {
-#define IK_X(M, X) hipLaunchKernelGGL((ann_fused_kernel<M, X>), dim3(grid), dim3(256), 0, st, a)
+#define IK_X(M, X) \
+  hipLaunchKernelGGL((ann_fused_kernel<M, X>), dim3(grid), dim3(64 * ann_waves<M, X>()), 0, st, a)
   if (mr == 2) {
     if (xmode == 2) IK_X(2, 2); else IK_X(2, 1);
   } else {
