@@ -810,12 +810,15 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 // the fp16x3 kernel at 64-point tiles runs IKHIP_ANN_XWAVES (default 8: two per
 // SIMD, NR = 2), so that one wave's weight loads and LDS reads issue under the
 // other's MFMAs.
+#ifndef IKHIP_ANN_BWAVES  // bf16x6: 8 waves measured 27.5 vs 25.6 ms (27 VGPR spills)
+#define IKHIP_ANN_BWAVES 4
+#endif
 #ifndef IKHIP_ANN_XWAVES
 #define IKHIP_ANN_XWAVES 8
 #endif
 template <int MR, int X>
 constexpr int ann_waves() {
-  return (X == 2 && MR == 2) ? IKHIP_ANN_XWAVES : kWaves;
+  return (X == 2 && MR == 2) ? IKHIP_ANN_XWAVES : (X == 1 && MR == 2) ? IKHIP_ANN_BWAVES : kWaves;
 }
 
 template <int MR, int X>
