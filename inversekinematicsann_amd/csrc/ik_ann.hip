@@ -813,12 +813,18 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 #ifndef IKHIP_ANN_BWAVES  // bf16x6: 8 waves measured 27.5 vs 25.6 ms (27 VGPR spills)
 #define IKHIP_ANN_BWAVES 4
 #endif
+#ifndef IKHIP_ANN_FWAVES  // fp32 at 64-point tiles (IKHIP_ANN_MR=2): 8 waves 40.9 ms, 4 41.6, MR=1 40.2
+#define IKHIP_ANN_FWAVES 4
+#endif
 #ifndef IKHIP_ANN_XWAVES
 #define IKHIP_ANN_XWAVES 8
 #endif
 template <int MR, int X>
 constexpr int ann_waves() {
-  return (X == 2 && MR == 2) ? IKHIP_ANN_XWAVES : (X == 1 && MR == 2) ? IKHIP_ANN_BWAVES : kWaves;
+  return (X == 2 && MR == 2)   ? IKHIP_ANN_XWAVES
+         : (X == 1 && MR == 2) ? IKHIP_ANN_BWAVES
+         : (X == 0 && MR == 2 && !kWide) ? IKHIP_ANN_FWAVES
+                                         : kWaves;
 }
 
 template <int MR, int X>
@@ -1165,7 +1171,8 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   if (xmode)
     launch_ann_kernel_x(mr, xmode, grid, st, a);
   else if (mr == 2)
-    hipLaunchKernelGGL((ann_fused_kernel<2, 0>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((ann_fused_kernel<2, 0>), dim3(grid), dim3(64 * ann_waves<2, 0>()), 0, st,
+                       a);
   else
     hipLaunchKernelGGL((ann_fused_kernel<1, 0>), dim3(grid), dim3(256), 0, st, a);
   kt_end(st);
