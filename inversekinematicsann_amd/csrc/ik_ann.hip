@@ -643,15 +643,8 @@ __device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WS
       c = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][1], sa[m].hi, c, 0, 0, 0);
       acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][0], sa[m].hi, c, 0, 0, 0);
     }
-  constexpr int kMfma = 3 * MR * NR, kLead = (kMfma >= 12) ? 6 : kMfma / 2;
-  __builtin_amdgcn_sched_group_barrier(0x020, 2 * NR, 0);  // VMEM reads
-  __builtin_amdgcn_sched_group_barrier(0x100, 2 * MR, 0);  // DS reads
-  __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
-#pragma unroll
-  for (int i = 0; i < kMfma - kLead; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-  }
+  // (no in-loop VALU left to interleave: with the split planes the compiler's own
+  // order of the loads and MFMAs measured 1.6 % faster than the bf16x6 pattern)
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int m = 0; m < MR; ++m) sa[m] = sn[m];
