@@ -684,27 +684,173 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
     for (int j = 0; j < NR; ++j) acc[m][j] *= xinv;
 }
 
+// fp16x3 on v_mfma_f32_16x16x32_f16 (IKHIP_ANN_H16, the default).  Same
+// products, same cycles per FLOP as the 32x32x16 form above, but the chip holds
+// a higher clock under the power cap on the 16x16 shape (MI355X_MICROARCH.md,
+// "Shape").  A wave's 32x32 tile (m, j) is four 16x16 sub-tiles s = 2 fh + ph
+// (feature half fh, point half ph), each in elements [4s, 4s + 4) of the f32x16
+// accumulator: lane l holds point 16 ph + (l & 15), features 32 nt + 16 fh +
+// 4 (l >> 4) + 0..3.  One K step is 32 deep: weights of plane p, feature half
+// fh at block ((g * 2 + fh) * 2 + p) of the tile (ann_pack_layer_h), and the
+// activations one ds_read_b128 per plane and point half.
+#ifndef IKHIP_ANN_H16
+#define IKHIP_ANN_H16 1
+#endif
+constexpr bool kH16 = IKHIP_ANN_H16 != 0;
+
+template <int NR>
+struct WStepH16 {
+  f16x8 p[NR][2][2];  // [tile][feature half][plane]
+};
+
+template <int NR>
+__device__ __forceinline__ void load_wh16(WStepH16<NR> &w, const WStream<NR> &ws, int g) {
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) w.p[j][fh][p] = wload<f16x8>(ws, j, (g * 2 + fh) * 2 + p);
+}
+
+// lane l: point 16 ph + (l & 15) of row group m, k 32 g + 8 (l >> 4) + 0..7
+template <int MR>
+__device__ __forceinline__ void load_ah16(Split2 (&a)[MR][2], const _Float16 *ap, int g) {
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      const _Float16 *q = ap + (m * 32 + 16 * ph) * 2 * kLd + 32 * g;
+      a[m][ph].hi = *reinterpret_cast<const f16x8 *>(q);
+      a[m][ph].lo = *reinterpret_cast<const f16x8 *>(q + 512);
+    }
+}
+
+template <int MR, int NR, int GI>
+__device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR> &w,
+                                         WStepH16<NR> &fill, const WStream<NR> &ws,
+                                         const _Float16 *ab, int g, f32x4 (&acc)[MR][NR][4]) {
+  __builtin_amdgcn_sched_barrier(0);
+  load_wh16(fill, ws, g + 1);
+  Split2 sn[MR][2];
+  load_ah16(sn, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+        for (int ph = 0; ph < 2; ++ph) {
+          f32x4 c = acc[m][j][2 * fh + ph];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].lo, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][1], sa[m][ph].hi, c, 0, 0, 0);
+          acc[m][j][2 * fh + ph] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].hi, c, 0, 0, 0);
+        }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
+}
+
+template <int MR, int NR, int W = kWaves>
+__device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__restrict__ wx,
+                                               int G32, int xbytes, float xinv, int wave, int lane,
+                                               const float *bias, f32x16 (&acc)[MR][NR]) {
+  const _Float16 *ap = hplane(const_cast<float *>(H), lane & 15) + 8 * (lane >> 4);
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
+  WStepH16<NR> w[2];
+  load_wh16(w[0], ws, 0);
+  f32x4 c4[MR][NR][4];
+  const float scale = 1.0f / xinv;  // exact: xinv is 2^-k
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh) {
+      const f32x4 b = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
+                                                        4 * (lane >> 4)) * scale;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) c4[m][j][2 * fh] = c4[m][j][2 * fh + 1] = b;
+    }
+  Split2 sa[MR][2];
+  load_ah16(sa, ap, 0);
+  int g = 0;
+  for (; g + 2 <= G32; g += 2) {
+    const _Float16 *ab = ap + 32 * g;
+    step_h16<MR, NR, 0>(sa, w[0], w[1], ws, ab, g, c4);
+    step_h16<MR, NR, 1>(sa, w[1], w[0], ws, ab, g + 1, c4);
+  }
+  if (g < G32) step_h16<MR, NR, 0>(sa, w[0], w[1], ws, ap + 32 * g, g, c4);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[m][j][4 * s + i] = c4[m][j][s][i] * xinv;
+}
+
+// Epilogue of an fp16x3 layer in the 16x16 sub-tile layout above: per lane and
+// sub-tile four consecutive features of one point, one 8-byte store per plane
+// (or one ds_write_b128 of fp32).
+template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
+__device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
+                                                f32x16 (&acc)[MR][NR], unsigned long long *st) {
+  stamp(st);
+  __syncthreads();  // every wave has finished reading the layer input
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh) {
+      const int col = (wave + W * j) * 32 + 16 * fh + 4 * (lane >> 4);
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        f32x2 t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = 4 * (2 * fh + (k >> 1)) + 2 * (k & 1);
+          t[k] = f32x2{acc[m][j][q], acc[m][j][q + 1]};
+        }
+        act_apply2x4<ACT>(t);
+#pragma unroll
+        for (int ph = 0; ph < 2; ++ph) {
+          const int row = m * 32 + 16 * ph + (lane & 15);
+          const f32x4 v = {t[2 * ph].x, t[2 * ph].y, t[2 * ph + 1].x, t[2 * ph + 1].y};
+          if constexpr (HOUT) store_h4(H, row, col, v);
+          else *reinterpret_cast<f32x4 *>(H + row * kLd + col) = v;
+        }
+      }
+    }
+}
+
 // One Dense layer for a wave with NR column tiles.  X: 0 fp32, 1 bf16x6,
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
 // a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
 // layer is one) stores the activations as split planes.
-template <int ACT, bool HOUT, int W, int MR, int NR>
+template <int ACT, bool HOUT, int W, int X, int MR, int NR>
 __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[NR], int wave,
                                           int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st) {
-  if (tr) layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
-  else layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
+  if (tr) {
+    if constexpr (X == 2 && kH16) layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
+    else layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
+  } else {
+    layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
+  }
 }
 
-template <bool HOUT, int W, int MR, int NR>
+template <bool HOUT, int W, int X, int MR, int NR>
 __device__ __forceinline__ void store_act(int act, bool tr, float *H, const float (&bv)[NR],
                                           int wave, int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st) {
   switch (act) {
-    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
-    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
-    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
-    default: store_any<IK_ACT_LINEAR, HOUT, W>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
+    default: store_any<IK_ACT_LINEAR, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
   }
 }
 
@@ -722,6 +868,9 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
     if (X == 1)
       layer_gemm_x<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024,
                               wave, lane, bias, acc);
+    else if constexpr (kH16)  // G16: 32-deep K steps here
+      layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
+                                xinv, wave, lane, bias, acc);
     else
       layer_gemm_h<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024,
                               xinv, wave, lane, bias, acc);
@@ -730,8 +879,8 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
     for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + W * j) * 32 + (lane & 31)];
     layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, W, lane, nullptr, acc, st_first);
   }
-  if (HX && hout) store_act<true, W>(act, tr, H, bv, wave, lane, acc, st);
-  else store_act<false, W>(act, tr, H, bv, wave, lane, acc, st);
+  if (HX && hout) store_act<true, W, X>(act, tr, H, bv, wave, lane, acc, st);
+  else store_act<false, W, X>(act, tr, H, bv, wave, lane, acc, st);
 }
 
 // HOUT: the next layer runs fp16x3, so the result goes out as split planes
@@ -878,7 +1027,8 @@ ann_fused_kernel(AnnArgs a) {
         run_layer_splitk<MR, X == 2, W>(H, wp, bias, act, G, wave, lane, tid, sl, hout);
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
-        const int G16 = (a.m.kp[l] + 15) >> 4;
+        // K steps of the split GEMM: 16 deep (bf16x6, 32x32x16 fp16x3), 32 (16x16x32)
+        const int G16 = (X == 2 && kH16) ? (a.m.kp[l] + 31) >> 5 : (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
@@ -1065,7 +1215,7 @@ void ann_pack_layer_x(const float *W, int k, int n, void *dst) {
 }
 
 size_t ann_h_bytes(int k, int n) {
-  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
+  int k16 = (k + (kH16 ? 31 : 15)) / (kH16 ? 32 : 16) * (kH16 ? 32 : 16), np = (n + 31) / 32 * 32;
   return (size_t)k16 * np * 4;
 }
 
@@ -1087,10 +1237,32 @@ int ann_h_scale_exp(const float *W, int k, int n) {
 // planes): dst[(((nt*G16 + g)*2 + p)*64 + l)*8 + j] = plane p of
 // W[16g + 8*(l>>5) + j][32nt + (l&31)] * 2^scale_exp, each plane rounded to
 // nearest (the scaled weight and its residual are exact in fp32).
+// With IKHIP_ANN_H16 (v_mfma_f32_16x16x32_f16, 32-deep K steps):
+// dst[((((nt*G32 + g)*2 + fh)*2 + p)*64 + l)*8 + j] = plane p of
+// W[32g + 8*(l>>4) + j][32nt + 16fh + (l&15)] * 2^scale_exp.
 void ann_pack_layer_h(const float *W, int k, int n, int scale_exp, void *dst) {
   int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
   int G16 = k16 / 16, NT = np / 32;
   _Float16 *d = static_cast<_Float16 *>(dst);
+  if (kH16) {
+    const int G32 = (k + 31) / 32;
+    for (int nt = 0; nt < NT; ++nt)
+      for (int g = 0; g < G32; ++g)
+        for (int fh = 0; fh < 2; ++fh)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+              const int kk = 32 * g + 8 * (lane >> 4) + j;
+              const int c = nt * 32 + 16 * fh + (lane & 15);
+              const float x =
+                  (kk < k && c < n) ? std::ldexp(W[(size_t)kk * n + c], scale_exp) : 0.0f;
+              const _Float16 h = (_Float16)x;
+              const size_t base =
+                  ((((size_t)nt * G32 + g) * 2 + fh) * 2) * 64 * 8 + (size_t)lane * 8 + j;
+              d[base] = h;
+              d[base + 64 * 8] = (_Float16)(x - (float)h);
+            }
+    return;
+  }
   for (int nt = 0; nt < NT; ++nt)
     for (int g = 0; g < G16; ++g)
       for (int lane = 0; lane < 64; ++lane)
