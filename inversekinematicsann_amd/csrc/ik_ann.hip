@@ -697,6 +697,9 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
 #define IKHIP_ANN_H16 1
 #endif
 constexpr bool kH16 = IKHIP_ANN_H16 != 0;
+#ifndef IKHIP_ANN_H16_PATTERN
+#define IKHIP_ANN_H16_PATTERN 0
+#endif
 
 template <int NR>
 struct WStepH16 {
@@ -748,6 +751,20 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
           acc[m][j][2 * fh + ph] =
               __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].hi, c, 0, 0, 0);
         }
+#if IKHIP_ANN_H16_PATTERN == 1
+  __builtin_amdgcn_sched_group_barrier(0x020, 4 * NR, 0);       // VMEM reads
+  __builtin_amdgcn_sched_group_barrier(0x100, 4 * MR, 0);       // DS reads
+  __builtin_amdgcn_sched_group_barrier(0x008, 12 * MR * NR, 0);  // MFMA
+#elif IKHIP_ANN_H16_PATTERN == 2
+  // one weight load, one LDS read per two MFMAs from the start of the step
+#pragma unroll
+  for (int i = 0; i < 4 * NR; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    if (i < 4 * MR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+  }
+#endif
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int m = 0; m < MR; ++m)

@@ -13,7 +13,7 @@ for f in $(git -C "$ROOT" ls-tree --name-only $REV inversekinematicsann_amd/csrc
   git -C "$ROOT" show $REV:$f > $T/a/csrc/$(basename $f)
 done
 cd $T/a/csrc
-FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off"
+FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $EXTRA"
 objs=""
 for o in ik_fk ik_fabrik ik_ann ik_ann_x ik_ann_w ik_shard; do
   /opt/rocm/bin/hipcc $FLAGS -c $o.hip -o $o.o & objs="$objs $o.o"
