@@ -697,8 +697,15 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
 #define IKHIP_ANN_H16 1
 #endif
 constexpr bool kH16 = IKHIP_ANN_H16 != 0;
+// weight-step buffers of the 16x16x32 loop (kH16Ring - 1 steps of 32 ahead)
+#ifndef IKHIP_ANN_H16_RING
+#define IKHIP_ANN_H16_RING 2
+#endif
+constexpr int kH16Ring = IKHIP_ANN_H16_RING;
+// 2: loads spread over the step's MFMAs (with 4 waves: 13.49 ms against 13.65 for
+// 8 waves in the compiler's order, 13.82 for 4 waves in it; 1 = loads first: 13.88)
 #ifndef IKHIP_ANN_H16_PATTERN
-#define IKHIP_ANN_H16_PATTERN 0
+#define IKHIP_ANN_H16_PATTERN 2
 #endif
 
 template <int NR>
@@ -734,7 +741,7 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
                                          WStepH16<NR> &fill, const WStream<NR> &ws,
                                          const _Float16 *ab, int g, f32x4 (&acc)[MR][NR][4]) {
   __builtin_amdgcn_sched_barrier(0);
-  load_wh16(fill, ws, g + 1);
+  load_wh16(fill, ws, g + kH16Ring - 1);
   Split2 sn[MR][2];
   load_ah16(sn, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
 #pragma unroll
@@ -778,8 +785,9 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
                                                const float *bias, f32x16 (&acc)[MR][NR]) {
   const _Float16 *ap = hplane(const_cast<float *>(H), lane & 15) + 8 * (lane >> 4);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
-  WStepH16<NR> w[2];
-  load_wh16(w[0], ws, 0);
+  WStepH16<NR> w[kH16Ring];
+#pragma unroll
+  for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
   f32x4 c4[MR][NR][4];
   const float scale = 1.0f / xinv;  // exact: xinv is 2^-k
 #pragma unroll
@@ -794,12 +802,19 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
   Split2 sa[MR][2];
   load_ah16(sa, ap, 0);
   int g = 0;
-  for (; g + 2 <= G32; g += 2) {
+  for (; g + kH16Ring <= G32; g += kH16Ring) {
     const _Float16 *ab = ap + 32 * g;
-    step_h16<MR, NR, 0>(sa, w[0], w[1], ws, ab, g, c4);
-    step_h16<MR, NR, 1>(sa, w[1], w[0], ws, ab, g + 1, c4);
+    static_for<kH16Ring>([&](auto u) {
+      step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
+                                g + u.value, c4);
+    });
   }
-  if (g < G32) step_h16<MR, NR, 0>(sa, w[0], w[1], ws, ap + 32 * g, g, c4);
+  const _Float16 *ab = ap + 32 * g;
+  static_for<kH16Ring - 1>([&](auto u) {
+    if (g + u.value < G32)
+      step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
+                                g + u.value, c4);
+  });
 #pragma unroll
   for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -975,8 +990,8 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 #ifndef IKHIP_ANN_FWAVES  // fp32 at 64-point tiles (IKHIP_ANN_MR=2): 8 waves 40.9 ms, 4 41.6, MR=1 40.2
 #define IKHIP_ANN_FWAVES 4
 #endif
-#ifndef IKHIP_ANN_XWAVES
-#define IKHIP_ANN_XWAVES 8
+#ifndef IKHIP_ANN_XWAVES  // 8 for the 32x32x16 loop (IKHIP_ANN_H16=0), 4 for 16x16x32
+#define IKHIP_ANN_XWAVES (IKHIP_ANN_H16 ? 4 : 8)
 #endif
 template <int MR, int X>
 constexpr int ann_waves() {
