@@ -708,6 +708,11 @@ constexpr int kH16Ring = IKHIP_ANN_H16_RING;
 #define IKHIP_ANN_H16_PATTERN 2
 #endif
 
+// IKHIP_EXP_L1W (timing experiment, wrong results): every step reads step 0's
+// blocks, which stay in L1 -- the weight stream without its L2 traffic.
+#ifndef IKHIP_EXP_L1W
+#define IKHIP_EXP_L1W 0
+#endif
 template <int NR>
 struct WStepH16 {
   f16x8 p[NR][2][2];  // [tile][feature half][plane]
@@ -720,7 +725,8 @@ __device__ __forceinline__ void load_wh16(WStepH16<NR> &w, const WStream<NR> &ws
 #pragma unroll
     for (int fh = 0; fh < 2; ++fh)
 #pragma unroll
-      for (int p = 0; p < 2; ++p) w.p[j][fh][p] = wload<f16x8>(ws, j, (g * 2 + fh) * 2 + p);
+      for (int p = 0; p < 2; ++p)
+        w.p[j][fh][p] = wload<f16x8>(ws, j, (IKHIP_EXP_L1W ? 0 : g * 4) + fh * 2 + p);
 }
 
 // lane l: point 16 ph + (l & 15) of row group m, k 32 g + 8 (l >> 4) + 0..7
