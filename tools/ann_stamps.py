@@ -20,6 +20,8 @@ ang = torch.empty((n, 4), dtype=torch.float32, device="cuda")
 err = torch.empty(n, dtype=torch.float64, device="cuda")
 ctx = _native.Context(0)
 ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+if __import__("os").environ.get("MODE"):  # fp32 (default) / bf16x6 / fp16x3
+    ctx.ann_set_mode(__import__("os").environ["MODE"])
 ctx.ann_solve_device(pts, ang, err, flags=_native.IK_F_DEVICE)
 ctx.set_debug(True)
 ctx.ann_solve_device(pts, ang, err, flags=_native.IK_F_DEVICE)
