@@ -785,45 +785,23 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
     for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
 }
 
-// Layer start (IKHIP_ANN_H16_PRE bits): 1 -- the bias joins after the K loop, so its
-// loads are not waited for before the first MFMA; 2 -- the first weight step of the
-// next layer (when it also runs this loop with the same tiles per wave) is loaded
-// before this layer's epilogue and handed over in registers.
-#ifndef IKHIP_ANN_H16_PRE
-#define IKHIP_ANN_H16_PRE 0
-#endif
-constexpr int kH16Pre = IKHIP_ANN_H16_PRE;
-template <int NR>
-struct H16Pre {
-  WStepH16<NR> w;
-  bool ok;
-};
-struct H16Next {
-  const f16x8 *wx;  // null: the next layer takes no prefetch
-  int G32, xbytes;
-};
-
 template <int MR, int NR, int W = kWaves>
 __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__restrict__ wx,
                                                int G32, int xbytes, float xinv, int wave, int lane,
-                                               const float *bias, f32x16 (&acc)[MR][NR],
-                                               H16Pre<NR> *pre = nullptr, H16Next nx = {}) {
+                                               const float *bias, f32x16 (&acc)[MR][NR]) {
   const _Float16 *ap = hplane(const_cast<float *>(H), lane & 15) + 8 * (lane >> 4);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
   WStepH16<NR> w[kH16Ring];
-  if ((kH16Pre & 2) && pre && pre->ok) w[0] = pre->w;
-  else load_wh16(w[0], ws, 0);
 #pragma unroll
-  for (int u = 1; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
-  f32x4 c4[MR][NR][4], bq[NR][2];
+  for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
+  f32x4 c4[MR][NR][4];
   const float scale = 1.0f / xinv;  // exact: xinv is 2^-k
 #pragma unroll
   for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int fh = 0; fh < 2; ++fh) {
-      bq[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
-                                                   4 * (lane >> 4));
-      const f32x4 b = (kH16Pre & 1) ? f32x4{0.0f, 0.0f, 0.0f, 0.0f} : bq[j][fh] * scale;
+      const f32x4 b = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
+                                                        4 * (lane >> 4)) * scale;
 #pragma unroll
       for (int m = 0; m < MR; ++m) c4[m][j][2 * fh] = c4[m][j][2 * fh + 1] = b;
     }
@@ -843,10 +821,6 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
       step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
                                 g + u.value, c4);
   });
-  if ((kH16Pre & 2) && pre) {
-    pre->ok = nx.wx != nullptr;
-    if (nx.wx) load_wh16(pre->w, make_wstream<NR>(nx.wx, nx.xbytes, wave, W, nx.G32 * 4, lane), 0);
-  }
 #pragma unroll
   for (int m = 0; m < MR; ++m)
 #pragma unroll
@@ -854,9 +828,7 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[m][j][4 * s + i] = (kH16Pre & 1) ? c4[m][j][s][i] * xinv + bq[j][s >> 1][i]
-                                               : c4[m][j][s][i] * xinv;
+        for (int i = 0; i < 4; ++i) acc[m][j][4 * s + i] = c4[m][j][s][i] * xinv;
 }
 
 // Epilogue of an fp16x3 layer in the 16x16 sub-tile layout above: per lane and
@@ -925,8 +897,7 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           unsigned long long *st_first,
                                           const void *wx = nullptr, int G16 = 0,
-                                          float xinv = 1.0f, bool hout = false,
-                                          H16Pre<NR> *pre = nullptr, H16Next nx = {}) {
+                                          float xinv = 1.0f, bool hout = false) {
   f32x16 acc[MR][NR];
   const int NT = wbytes / (G * 1024);  // column tiles of the layer
   float bv[NR];
@@ -937,7 +908,7 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
                               wave, lane, bias, acc);
     else if constexpr (kH16)  // G16: 32-deep K steps here
       layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
-                                xinv, wave, lane, bias, acc, pre, nx);
+                                xinv, wave, lane, bias, acc);
     else
       layer_gemm_h<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024,
                               xinv, wave, lane, bias, acc);
@@ -1047,8 +1018,6 @@ ann_fused_kernel(AnnArgs a) {
   const int wave = tid >> 6, lane = tid & 63;
   const int64_t ntiles = (a.n + BM - 1) / BM;
   double blk_max = 0.0, blk_sum = 0.0;  // FK round-trip error of this lane's points
-  H16Pre<4> pre4;  // fp16x3 16x16x32: the next layer's first weight step (kH16Pre & 2)
-  pre4.ok = false;
 
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t pt = tile * BM + tid;
@@ -1099,22 +1068,9 @@ ann_fused_kernel(AnnArgs a) {
         // K steps of the split GEMM: 16 deep (bf16x6, 32x32x16 fp16x3), 32 (16x16x32)
         const int G16 = (X == 2 && kH16) ? (a.m.kp[l] + 31) >> 5 : (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
-        H16Next nx{};  // the next layer's operand, when it takes the prefetch
-        if constexpr (X == 2 && kH16 && (kH16Pre & 2)) {
-          const int ln = l + 1;
-          if (ln < a.m.n_layers && a.m.wx[ln]) {
-            const int NTn = a.m.np[ln] >> 5;
-            const int cntn = (wave < NTn) ? (NTn - wave + W - 1) / W : 0;
-            if (NTn > 1 && cntn == cnt) {
-              nx.wx = static_cast<const f16x8 *>(a.m.wx[ln]);
-              nx.G32 = (a.m.kp[ln] + 31) >> 5;
-              nx.xbytes = NTn * nx.G32 * 4 * 1024;
-            }
-          }
-        }
         switch (cnt) {
           case 4:
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout, &pre4, nx);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
             break;
           case 3:
             if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
