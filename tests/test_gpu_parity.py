@@ -565,10 +565,12 @@ def test_cli_call_uploads_the_robot_at_most_once():
     assert int(line[0].split()[1]) <= 1
 
 
-def test_ann_tile_variants_agree(ctx1, tmp_path):
+@pytest.mark.parametrize("mode", ["fp32", "bf16x6", "fp16x3"])
+def test_ann_tile_variants_agree(ctx1, tmp_path, mode):
     """fp32 runs 32-point tiles by default (MR = 1), the split modes 64 (MR = 2);
     IKHIP_ANN_MR forces either.  The other tile size, in a fresh process, gives
-    the same bits (per point the same K order and the same fixed split-K sum)."""
+    the same bits (per point the same K order and the same fixed split-K sum) --
+    for fp16x3 also through the 16x16x32 sub-tiles of a 32-point tile."""
     import subprocess
     import sys
     from tests.conftest import ROOT
@@ -579,8 +581,12 @@ def test_ann_tile_variants_agree(ctx1, tmp_path):
     m = glorot_model(dims=dims, seed=9)
     pts = random_dist(5000, seed=9)
     ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
-    mine, err, _ = ctx1.ann_solve(pts, want_fk_err=True)
-    out = tmp_path / "mr2.npz"
+    ctx1.ann_set_mode(mode)
+    try:
+        mine, err, _ = ctx1.ann_solve(pts, want_fk_err=True)
+    finally:
+        ctx1.ann_set_mode("fp32")
+    out = tmp_path / "other.npz"
     code = (
         "import numpy as np\n"
         "from inversekinematicsann_amd import _native\n"
@@ -590,10 +596,12 @@ def test_ann_tile_variants_agree(ctx1, tmp_path):
         f"m = glorot_model(dims={dims!r}, seed=9); pts = random_dist(5000, seed=9)\n"
         "c = _native.Context(0)\n"
         "c.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)\n"
+        f"c.ann_set_mode({mode!r})\n"
         "a, e, _ = c.ann_solve(pts, want_fk_err=True)\n"
         f"np.savez({str(out)!r}, a=a, e=e)\n")
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
-                       timeout=120, env=dict(os.environ, IKHIP_ANN_MR="2"))
+                       timeout=120,
+                       env=dict(os.environ, IKHIP_ANN_MR="2" if mode == "fp32" else "1"))
     assert r.returncode == 0, r.stderr[-2000:]
     other = np.load(out)
     assert np.array_equal(mine, other["a"]) and np.array_equal(err, other["e"])
