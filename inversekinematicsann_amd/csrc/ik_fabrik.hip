@@ -367,7 +367,10 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
 // -> scatter (class region starts from the totals, one cursor per class: the
 // queue -> point permutation) -> iterate (the last block to finish folds this
 // call's records into the table for the next call).
-constexpr int kOrdPPT = 8;  // points per thread of the classify / scatter blocks
+#ifndef IKHIP_ORD_PPT
+#define IKHIP_ORD_PPT 8
+#endif
+constexpr int kOrdPPT = IKHIP_ORD_PPT;  // points per thread of the classify / scatter blocks
 
 // The shoulder (the seed's first joint, the translation of A_1) is
 // (a1 cos t1, a1 sin t1, d1) with t1 the goal's own azimuth: its distance from the
@@ -384,12 +387,19 @@ __device__ __forceinline__ int goal_cell(const RobotDev &r, d3 g) {
   return rb * kOrdCellsE + eb;
 }
 
-__device__ __forceinline__ int cost_class(const FabOrderDev *T, int cell, int max_iter) {
-  const unsigned int key = T->key[cell];  // 1 + largest recorded iterations, 0 = unseen
+__device__ __forceinline__ int key_class(unsigned int key, int max_iter) {
+  // key: 1 + largest recorded iterations, 0 = unseen
   if (key == 0) return kOrdClasses - 1;
   const int k = (int)((long long)(key - 1) * kOrdClasses / (max_iter + 1));
   return k < 0 ? 0 : (k >= kOrdClasses ? kOrdClasses - 1 : k);
 }
+
+__device__ __forceinline__ int cost_class(const FabOrderDev *T, int cell, int max_iter) {
+  return key_class(T->key[cell], max_iter);
+}
+#ifndef IKHIP_ORD_EARLY
+#define IKHIP_ORD_EARLY 1
+#endif
 
 // Fold ns records into the table: per cell, the largest recorded iteration
 // count of the call, or the decayed old key if larger.  One block.
@@ -428,8 +438,6 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
   __shared__ unsigned int cnt[kOrdClasses];
   __shared__ uint8_t cls[kOrdCells];
   const int t = threadIdx.x;
-  if (t < kOrdClasses) cnt[t] = 0;
-  for (int c = t; c < kOrdCells; c += 256) cls[c] = (uint8_t)cost_class(a.ord, c, a.max_iter);
   const int64_t b0 = (int64_t)blockIdx.x * (256 * kOrdPPT);
   d3 g[kOrdPPT];
 #pragma unroll
@@ -437,6 +445,18 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
     const int64_t i = b0 + j * 256 + t;
     if (i < a.n) g[j] = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
   }
+  if (t < kOrdClasses) cnt[t] = 0;
+#if IKHIP_ORD_EARLY
+  // the cell -> class map's table reads in flight with the goals'
+  unsigned int key[kOrdCells / 256];
+#pragma unroll
+  for (int q = 0; q < kOrdCells / 256; ++q) key[q] = a.ord->key[t + 256 * q];
+#pragma unroll
+  for (int q = 0; q < kOrdCells / 256; ++q)
+    cls[t + 256 * q] = (uint8_t)key_class(key[q], a.max_iter);
+#else
+  for (int c = t; c < kOrdCells; c += 256) cls[c] = (uint8_t)cost_class(a.ord, c, a.max_iter);
+#endif
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kOrdPPT; ++j) {
