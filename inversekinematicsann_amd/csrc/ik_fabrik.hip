@@ -474,9 +474,6 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
   if (t < kOrdClasses && cnt[t]) atomicAdd(&a.S->cls_tot[t][blockIdx.x % kOrdShards], cnt[t]);
 }
 
-#ifndef IKHIP_ORD_ROWSYNC
-#define IKHIP_ORD_ROWSYNC 1
-#endif
 // 2. scatter: perm[queue position] = point.  The queue is class-major (hardest
 // first), then shard: region (c, s) starts after every harder class and every
 // lower shard of class c.  Block b covers the points classify's block b counted
@@ -523,12 +520,6 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
       const unsigned int pos = atomicAdd(&base[cl[j] >> 10], 1u);
       a.perm[pos] = (int32_t)(b0 + j * 256 + t);
     }
-#if IKHIP_ORD_ROWSYNC
-    // rows of 256 points claim their slots one after the other, so a class's run
-    // follows point order row by row: a grab's 64 points then share the cache
-    // lines of their goals and results
-    __syncthreads();
-#endif
   }
 }
 
