@@ -451,31 +451,38 @@ def end_to_end(job, solve_host, args):
     reps = max(1, min(args.steps, 10))
 
     def rate(host_pts, pinned):
-        # untimed warm-up: the staging scratch, the pipeline's streams, and the
-        # copy engines' queues, which the runtime sets up over the first calls (the
-        # first pinned calls of a process measured 19-22 / 7.7-10 / 1.2-8.3 ms,
-        # steady 1.10-1.13: tools/pinned_probe.py)
-        for _ in range(5):
+        # untimed warm-up (10 calls): the staging scratch, the pipeline's streams,
+        # and the copy engines' queues, which the runtime sets up over the first
+        # calls (the first pinned calls of a process measured 19-22 / 7.7-10 /
+        # 1.2-8.3 ms, steady 1.10-1.13: tools/pinned_probe.py)
+        for _ in range(10):
             solve_host(host_pts, pinned)
         barrier(job.world)
         t0 = time.perf_counter()
+        calls = []  # this rank's per-call times (the host path returns when D2H is done)
         for _ in range(reps):
+            t1 = time.perf_counter()
             solve_host(host_pts, pinned)
+            calls.append((time.perf_counter() - t1) * 1e3)
         torch.cuda.synchronize()
         barrier(job.world)
         wall = max_over_ranks(time.perf_counter() - t0, job.world)
-        return wall * 1e3 / reps
+        return wall * 1e3 / reps, float(np.median(calls)), float(max(calls))
 
     pp = _native.pinned_empty(pts.shape, np.float64)
     pp[:] = pts
-    ms = rate(pp, True)
-    ms_pageable = rate(np.ascontiguousarray(pts), False)
+    ms, med, mx = rate(pp, True)
+    ms_pageable, med_p, mx_p = rate(np.ascontiguousarray(pts), False)
+    # ms_per_step / value: the mean over the timed calls; median / max per call
+    # beside it (the runtime's pinned copies have occasional multi-ms outliers)
     return {"ms_per_step": ms, "value": job.total / (ms / 1e3), "steps": reps,
+            "median_ms": med, "max_ms": mx,
             "unit": "IK solutions/s",
             "path": "host pointers (ik_*_solve without IK_F_DEVICE), pinned host arrays "
                     "(ik_host_alloc; chunked copy/compute overlap)",
             "pageable": {"ms_per_step": ms_pageable,
-                         "value": job.total / (ms_pageable / 1e3)}}
+                         "value": job.total / (ms_pageable / 1e3),
+                         "median_ms": med_p, "max_ms": mx_p}}
 
 
 def _host_cpu():
