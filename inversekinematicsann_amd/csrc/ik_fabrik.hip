@@ -396,12 +396,6 @@ __device__ __forceinline__ int key_class(unsigned int key, int max_iter) {
   return k < 0 ? 0 : (k >= kOrdClasses ? kOrdClasses - 1 : k);
 }
 
-__device__ __forceinline__ int cost_class(const FabOrderDev *T, int cell, int max_iter) {
-  return key_class(T->key[cell], max_iter);
-}
-#ifndef IKHIP_ORD_EARLY
-#define IKHIP_ORD_EARLY 1
-#endif
 
 // Fold ns records into the table: per cell, the largest recorded iteration
 // count of the call, or the decayed old key if larger.  One block.
@@ -448,17 +442,14 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
     if (i < a.n) g[j] = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
   }
   if (t < kOrdClasses) cnt[t] = 0;
-#if IKHIP_ORD_EARLY
-  // the cell -> class map's table reads in flight with the goals'
+  // the cell -> class map's table reads, in flight with the goals'
+  static_assert(kOrdCells % 256 == 0, "whole table rows per thread");
   unsigned int key[kOrdCells / 256];
 #pragma unroll
   for (int q = 0; q < kOrdCells / 256; ++q) key[q] = a.ord->key[t + 256 * q];
 #pragma unroll
   for (int q = 0; q < kOrdCells / 256; ++q)
     cls[t + 256 * q] = (uint8_t)key_class(key[q], a.max_iter);
-#else
-  for (int c = t; c < kOrdCells; c += 256) cls[c] = (uint8_t)cost_class(a.ord, c, a.max_iter);
-#endif
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kOrdPPT; ++j) {
