@@ -777,13 +777,6 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
     if (i < 4 * MR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
   }
-#elif IKHIP_ANN_H16_PATTERN == 3
-  // only the LDS reads spread (one per 6 MFMAs), the weight loads where the compiler puts them
-#pragma unroll
-  for (int i = 0; i < 4 * MR; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
-  }
 #endif
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
