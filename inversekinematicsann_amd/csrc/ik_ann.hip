@@ -986,10 +986,11 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 // X: 0 fp32; 1 bf16x6, 2 fp16x3 -- layers whose split weight operand exists
 // (a.m.wx[l]) take the split GEMM; the others (input layer, split-K output
 // layer, fp16x3-ineligible layers) stay fp32.
-// Waves per workgroup: 4, one per SIMD (NR column tiles each, 4 at full width);
-// the fp16x3 kernel at 64-point tiles runs IKHIP_ANN_XWAVES (default 8: two per
-// SIMD, NR = 2), so that one wave's weight loads and LDS reads issue under the
-// other's MFMAs.
+// Waves per workgroup: 4, one per SIMD (NR column tiles each, 4 at full width).
+// IKHIP_ANN_XWAVES for the fp16x3 kernel at 64-point tiles: 4 with the 16x16x32
+// loop (its loads spread over the MFMAs, pattern 2: 13.34 against 13.59 ms for 8),
+// 8 with the 32x32x16 loop (two per SIMD, NR = 2: one wave's weight loads and LDS
+// reads issue under the other's MFMAs).
 #ifndef IKHIP_ANN_BWAVES  // bf16x6: 8 waves measured 27.5 vs 25.6 ms (27 VGPR spills)
 #define IKHIP_ANN_BWAVES 4
 #endif
