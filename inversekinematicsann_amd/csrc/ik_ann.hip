@@ -576,9 +576,11 @@ __device__ __forceinline__ void static_for(F &&f) {
 // Opt-in (IK_ANN_FP16X3): x = hi + lo in fp16 (round to nearest; the residual
 // is exact in fp32), weights pre-scaled by 2^k so their largest is ~2^14, and
 // the three products above 2^-22 -- lo*hi, hi*lo, hi*hi -- accumulated in fp32
-// by v_mfma_f32_32x32x16_f16 (fp16 products are exact in fp32); the result is
-// scaled back by 2^-k (exact).  3 MFMAs (96 cycles) per 32x32x16 block against
-// 6 for bf16x6 and 8 fp32 ones (512 cycles), 4 B per weight from L2.  Only for
+// by v_mfma_f32_16x16x32_f16 (layer_gemm_h16, the default) or
+// v_mfma_f32_32x32x16_f16 (layer_gemm_h, IKHIP_ANN_H16=0); fp16 products are
+// exact in fp32.  The result is scaled back by 2^-k (exact).  3 MFMAs (96
+// cycles) per 32x32x16 block against 6 for bf16x6 and 8 fp32 ones (512
+// cycles), 4 B per weight from L2.  Only for
 // layers whose input is bounded (the layer before is tanh or sigmoid): fp16's
 // range ends at 65504.  Accuracy on the reference architecture: max |d| to a
 // float64 forward 3.6e-7, the same as numpy's float32 forward (test_gpu_parity).
