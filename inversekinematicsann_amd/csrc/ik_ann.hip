@@ -866,6 +866,141 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
     }
 }
 
+// bf16x6 on v_mfma_f32_16x16x32_bf16 (IKHIP_ANN_X16): the same six products in
+// the 16x16 sub-tile layout of layer_gemm_h16 (epilogue layer_store_h16), the
+// activations split in VALU as they are read: lane l reads point 16 ph + (l & 15)
+// of row group m, k 32 g + 8 (l >> 4) + 0..7 (two ds_read_b128).  Weights: plane p
+// of feature half fh at block ((g * 2 + fh) * 3 + p) of the tile (ann_pack_layer_x).
+#ifndef IKHIP_ANN_X16
+#define IKHIP_ANN_X16 0
+#endif
+constexpr bool kX16 = IKHIP_ANN_X16 != 0;
+#ifndef IKHIP_ANN_X16_PATTERN
+#define IKHIP_ANN_X16_PATTERN 1
+#endif
+
+template <int NR>
+struct WStepX16 {
+  bf16x8 p[NR][2][3];  // [tile][feature half][plane]
+};
+
+template <int NR>
+__device__ __forceinline__ void load_wx16(WStepX16<NR> &w, const WStream<NR> &ws, int g) {
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) w.p[j][fh][p] = wload<bf16x8>(ws, j, (g * 2 + fh) * 3 + p);
+}
+
+template <int MR>
+__device__ __forceinline__ void load_ax16(f32x8 (&a)[MR][2], const float *ap, int g) {
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      const f32x4 *q = reinterpret_cast<const f32x4 *>(ap + (m * 32 + 16 * ph) * kLd + 32 * g);
+      const f32x4 lo4 = q[0], hi4 = q[1];
+      a[m][ph] = f32x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
+    }
+}
+
+template <int MR, int NR, int GI>
+__device__ __forceinline__ void step_x16(Split3 (&sa)[MR][2], const WStepX16<NR> &w,
+                                         WStepX16<NR> &fill, const WStream<NR> &ws,
+                                         const float *ab, int g, f32x4 (&acc)[MR][NR][4]) {
+  __builtin_amdgcn_sched_barrier(0);
+  load_wx16(fill, ws, g + 1);
+  f32x8 an[MR][2];
+  load_ax16(an, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
+  Split3 sn[MR][2];
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) sn[m][ph] = split3(an[m][ph]);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+        for (int ph = 0; ph < 2; ++ph) {
+          const bf16x8 *wp = w.p[j][fh];
+          const Split3 &x = sa[m][ph];
+          f32x4 c = acc[m][j][2 * fh + ph];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[0], x.lo, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[1], x.mid, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[2], x.hi, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[0], x.mid, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[1], x.hi, c, 0, 0, 0);
+          acc[m][j][2 * fh + ph] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[0], x.hi, c, 0, 0, 0);
+        }
+#if IKHIP_ANN_X16_PATTERN
+  // the loads, a few MFMAs to cover the LDS latency, then the split VALU two
+  // instructions per MFMA gap (as step_x)
+  constexpr int kMfma = 24 * MR * NR, kLead = 6;
+  __builtin_amdgcn_sched_group_barrier(0x020, 6 * NR, 0);  // VMEM reads
+  __builtin_amdgcn_sched_group_barrier(0x100, 4 * MR, 0);  // DS reads
+  __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
+#pragma unroll
+  for (int i = 0; i < kMfma - kLead; ++i) {
+    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+  }
+#endif
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
+}
+
+template <int MR, int NR, int W = kWaves>
+__device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__restrict__ wx,
+                                               int G32, int xbytes, int wave, int lane,
+                                               const float *bias, f32x16 (&acc)[MR][NR]) {
+  const float *ap = H + (lane & 15) * kLd + 8 * (lane >> 4);
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 6, lane);
+  WStepX16<NR> w[2];
+  load_wx16(w[0], ws, 0);
+  f32x4 c4[MR][NR][4];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh) {
+      const f32x4 b = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
+                                                        4 * (lane >> 4));
+#pragma unroll
+      for (int m = 0; m < MR; ++m) c4[m][j][2 * fh] = c4[m][j][2 * fh + 1] = b;
+    }
+  Split3 sa[MR][2];
+  {
+    f32x8 a0[MR][2];
+    load_ax16(a0, ap, 0);
+#pragma unroll
+    for (int m = 0; m < MR; ++m)
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) sa[m][ph] = split3(a0[m][ph]);
+  }
+  int g = 0;
+  for (; g + 2 <= G32; g += 2) {
+    const float *ab = ap + 32 * g;
+    step_x16<MR, NR, 0>(sa, w[0], w[1], ws, ab, g, c4);
+    step_x16<MR, NR, 1>(sa, w[1], w[0], ws, ab, g + 1, c4);
+  }
+  if (g < G32) step_x16<MR, NR, 0>(sa, w[0], w[1], ws, ap + 32 * g, g, c4);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[m][j][4 * s + i] = c4[m][j][s][i];
+}
+
 // One Dense layer for a wave with NR column tiles.  X: 0 fp32, 1 bf16x6,
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
 // a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
@@ -875,7 +1010,8 @@ __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[N
                                           int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st) {
   if (tr) {
-    if constexpr (X == 2 && kH16) layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
+    if constexpr ((X == 2 && kH16) || (X == 1 && kX16))
+      layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
     else layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
   } else {
     layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
@@ -905,9 +1041,14 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   float bv[NR];
   const bool tr = X != 0 && wx;  // split GEMM: transposed tile, bias in the accumulators
   if (tr) {
-    if (X == 1)
-      layer_gemm_x<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024,
-                              wave, lane, bias, acc);
+    if (X == 1) {
+      if constexpr (kX16)  // G16: 32-deep K steps here
+        layer_gemm_x16<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 6 * 1024,
+                                  wave, lane, bias, acc);
+      else
+        layer_gemm_x<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024,
+                                wave, lane, bias, acc);
+    }
     else if constexpr (kH16)  // G16: 32-deep K steps here
       layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
                                 xinv, wave, lane, bias, acc);
@@ -1069,7 +1210,8 @@ ann_fused_kernel(AnnArgs a) {
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
         // K steps of the split GEMM: 16 deep (bf16x6, 32x32x16 fp16x3), 32 (16x16x32)
-        const int G16 = (X == 2 && kH16) ? (a.m.kp[l] + 31) >> 5 : (a.m.kp[l] + 15) >> 4;
+        const int G16 =
+            ((X == 2 && kH16) || (X == 1 && kX16)) ? (a.m.kp[l] + 31) >> 5 : (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
@@ -1207,7 +1349,7 @@ void ann_pack_layer(const float *W, int k, int n, float *dst) {
 }
 
 size_t ann_x_bytes(int k, int n) {
-  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
+  int k16 = (k + (kX16 ? 31 : 15)) / (kX16 ? 32 : 16) * (kX16 ? 32 : 16), np = (n + 31) / 32 * 32;
   return (size_t)k16 * np * 6;
 }
 
@@ -1237,6 +1379,28 @@ void ann_pack_layer_x(const float *W, int k, int n, void *dst) {
   int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
   int G16 = k16 / 16, NT = np / 32;
   uint16_t *d16 = static_cast<uint16_t *>(dst);
+  if (kX16) {  // 16x16x32 order: dst[((((nt*G32 + g)*2 + fh)*3 + p)*64 + l)*8 + j]
+    const int G32 = (k + 31) / 32;
+    for (int nt = 0; nt < NT; ++nt)
+      for (int g = 0; g < G32; ++g)
+        for (int fh = 0; fh < 2; ++fh)
+          for (int lane = 0; lane < 64; ++lane)
+            for (int j = 0; j < 8; ++j) {
+              const int kk = 32 * g + 8 * (lane >> 4) + j;
+              const int c = nt * 32 + 16 * fh + (lane & 15);
+              const float x = (kk < k && c < n) ? W[(size_t)kk * n + c] : 0.0f;
+              const uint16_t h = bf16_rne(x);
+              const float r1 = x - bf16_to_f32(h);
+              const uint16_t m = bf16_rne(r1);
+              const float r2 = r1 - bf16_to_f32(m);
+              const size_t base =
+                  ((((size_t)nt * G32 + g) * 2 + fh) * 3) * 64 * 8 + (size_t)lane * 8 + j;
+              d16[base] = h;
+              d16[base + 64 * 8] = m;
+              d16[base + 2 * 64 * 8] = bf16_rne(r2);
+            }
+    return;
+  }
   for (int nt = 0; nt < NT; ++nt)
     for (int g = 0; g < G16; ++g)
       for (int lane = 0; lane < 64; ++lane)
