@@ -941,11 +941,14 @@ __device__ __forceinline__ void step_x16(Split3 (&sa)[MR][2], const WStepX16<NR>
   // the loads, a few MFMAs to cover the LDS latency, then the split VALU two
   // instructions per MFMA gap (as step_x)
   constexpr int kMfma = 24 * MR * NR, kLead = 6;
-  __builtin_amdgcn_sched_group_barrier(0x020, 6 * NR, 0);  // VMEM reads
+  if (IKHIP_ANN_X16_PATTERN == 1)
+    __builtin_amdgcn_sched_group_barrier(0x020, 6 * NR, 0);  // VMEM reads, all first
   __builtin_amdgcn_sched_group_barrier(0x100, 4 * MR, 0);  // DS reads
   __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
 #pragma unroll
   for (int i = 0; i < kMfma - kLead; ++i) {
+    if (IKHIP_ANN_X16_PATTERN == 2 && i % 2 == 0 && i / 2 < 6 * NR)
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read, spread
     __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
   }
