@@ -871,8 +871,11 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
 // activations split in VALU as they are read: lane l reads point 16 ph + (l & 15)
 // of row group m, k 32 g + 8 (l >> 4) + 0..7 (two ds_read_b128).  Weights: plane p
 // of feature half fh at block ((g * 2 + fh) * 3 + p) of the tile (ann_pack_layer_x).
+// Same box: 26.26 -> 24.12 ms per 1M points with the loads first (pattern 1, 40
+// VGPRs spilled outside the loop); 25.18 in the compiler's order (0, no spills);
+// weight loads spread (2): 23.5 against 23.1 for 1 on another box.
 #ifndef IKHIP_ANN_X16
-#define IKHIP_ANN_X16 0
+#define IKHIP_ANN_X16 1
 #endif
 constexpr bool kX16 = IKHIP_ANN_X16 != 0;
 #ifndef IKHIP_ANN_X16_PATTERN
