@@ -946,12 +946,8 @@ __device__ __forceinline__ void step_x16(Split3 (&sa)[MR][2], const WStepX16<NR>
   constexpr int kMfma = 24 * MR * NR, kLead = 6;
   if (IKHIP_ANN_X16_PATTERN == 1)
     __builtin_amdgcn_sched_group_barrier(0x020, 6 * NR, 0);  // VMEM reads, all first
-  if (IKHIP_ANN_X16_PATTERN == 3)
-    __builtin_amdgcn_sched_group_barrier(0x020, 3 * NR, 0);  // VMEM reads, half first
   __builtin_amdgcn_sched_group_barrier(0x100, 4 * MR, 0);  // DS reads
   __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
-  if (IKHIP_ANN_X16_PATTERN == 3)
-    __builtin_amdgcn_sched_group_barrier(0x020, 3 * NR, 0);  // and the other half
 #pragma unroll
   for (int i = 0; i < kMfma - kLead; ++i) {
     if (IKHIP_ANN_X16_PATTERN == 2 && i % 2 == 0 && i / 2 < 6 * NR)
