@@ -1007,74 +1007,6 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
         for (int i = 0; i < 4; ++i) acc[m][j][4 * s + i] = c4[m][j][s][i];
 }
 
-// fp16x3 16x16x32 with the epilogue's activation under the MFMAs
-// (IKHIP_ANN_H16_OVERLAP, 8 waves: two per SIMD, waves w and w + 4 on one SIMD).
-// The activation is bound by quarter-rate transcendentals and, with every wave in
-// the same phase, runs while the MFMA pipe idles.  Here a wave takes its column
-// tiles one K loop each, and the two waves of a SIMD order their work differently:
-// waves 0-3 activate each tile right after its K loop, waves 4-7 run all their K
-// loops first -- so one wave's transcendentals issue while the other's MFMAs run.
-// The activated values stay in registers until every wave has read the layer's
-// input (the barrier), then go out as the usual stores.  The price: each tile's K
-// loop reads the activations from LDS again (NR times the LDS reads).
-#ifndef IKHIP_ANN_H16_OVERLAP
-#define IKHIP_ANN_H16_OVERLAP 0
-#endif
-constexpr bool kH16Overlap = IKHIP_ANN_H16_OVERLAP != 0;
-
-template <int ACT, int MR>
-__device__ __forceinline__ void act_tile(f32x16 (&a)[MR][1]) {
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int q0 = 0; q0 < 16; q0 += 8) {
-      f32x2 t[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) t[k] = f32x2{a[m][0][q0 + 2 * k], a[m][0][q0 + 2 * k + 1]};
-      act_apply2x4<ACT>(t);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        a[m][0][q0 + 2 * k] = t[k].x;
-        a[m][0][q0 + 2 * k + 1] = t[k].y;
-      }
-    }
-}
-
-template <int MR, int NR, int ACT, bool HOUT, int W>
-__device__ __forceinline__ void layer_h16_overlap(float *H, const f16x8 *__restrict__ wx, int G32,
-                                                  int xbytes, float xinv, int wave, int lane,
-                                                  const float *bias, unsigned long long *st) {
-  f32x16 acc[NR][MR][1];
-  const bool late = wave >= 4;  // the second wave of its SIMD
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    layer_gemm_h16<MR, 1, W>(H, wx, G32, xbytes, xinv, wave + W * j, lane, bias, acc[j]);
-    if (!late) act_tile<ACT>(acc[j]);
-  }
-  if (late) {
-#pragma unroll
-    for (int j = 0; j < NR; ++j) act_tile<ACT>(acc[j]);
-  }
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    if (j == 0) layer_store_h16<MR, 1, IK_ACT_LINEAR, HOUT, W>(H, wave, lane, acc[0], st);
-    else layer_store_h16<MR, 1, IK_ACT_LINEAR, HOUT, W>(H, wave + W * j, lane, acc[j], nullptr);
-  }
-}
-
-template <int MR, int NR, bool HOUT, int W>
-__device__ __forceinline__ void layer_h16_overlap_act(int act, float *H, const f16x8 *wx, int G32,
-                                                      int xbytes, float xinv, int wave, int lane,
-                                                      const float *bias,
-                                                      unsigned long long *st) {
-  switch (act) {
-    case IK_ACT_TANH: layer_h16_overlap<MR, NR, IK_ACT_TANH, HOUT, W>(H, wx, G32, xbytes, xinv, wave, lane, bias, st); break;
-    case IK_ACT_RELU: layer_h16_overlap<MR, NR, IK_ACT_RELU, HOUT, W>(H, wx, G32, xbytes, xinv, wave, lane, bias, st); break;
-    case IK_ACT_SIGMOID: layer_h16_overlap<MR, NR, IK_ACT_SIGMOID, HOUT, W>(H, wx, G32, xbytes, xinv, wave, lane, bias, st); break;
-    default: layer_h16_overlap<MR, NR, IK_ACT_LINEAR, HOUT, W>(H, wx, G32, xbytes, xinv, wave, lane, bias, st); break;
-  }
-}
-
 // One Dense layer for a wave with NR column tiles.  X: 0 fp32, 1 bf16x6,
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
 // a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
@@ -1110,22 +1042,10 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
                                           unsigned long long *st_first,
                                           const void *wx = nullptr, int G16 = 0,
                                           float xinv = 1.0f, bool hout = false) {
-  const int NT = wbytes / (G * 1024);  // column tiles of the layer
-  const bool tr = X != 0 && wx;  // split GEMM: transposed tile, bias in the accumulators
-  if constexpr (X == 2 && kH16 && kH16Overlap && W == 8) {
-    if (tr) {
-      const f16x8 *xw = static_cast<const f16x8 *>(wx);
-      if (HX && hout)
-        layer_h16_overlap_act<MR, NR, true, W>(act, H, xw, G16, NT * G16 * 4 * 1024, xinv, wave,
-                                               lane, bias, st);
-      else
-        layer_h16_overlap_act<MR, NR, false, W>(act, H, xw, G16, NT * G16 * 4 * 1024, xinv, wave,
-                                                lane, bias, st);
-      return;
-    }
-  }
   f32x16 acc[MR][NR];
+  const int NT = wbytes / (G * 1024);  // column tiles of the layer
   float bv[NR];
+  const bool tr = X != 0 && wx;  // split GEMM: transposed tile, bias in the accumulators
   if (tr) {
     if (X == 1) {
       if constexpr (kX16)  // G16: 32-deep K steps here
@@ -1227,7 +1147,7 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 #define IKHIP_ANN_FWAVES 4
 #endif
 #ifndef IKHIP_ANN_XWAVES  // 8 for the 32x32x16 loop (IKHIP_ANN_H16=0), 4 for 16x16x32
-#define IKHIP_ANN_XWAVES ((IKHIP_ANN_H16 && !IKHIP_ANN_H16_OVERLAP) ? 4 : 8)
+#define IKHIP_ANN_XWAVES (IKHIP_ANN_H16 ? 4 : 8)
 #endif
 template <int MR, int X>
 constexpr int ann_waves() {
