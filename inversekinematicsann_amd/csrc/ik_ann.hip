@@ -790,7 +790,8 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
 template <int MR, int NR, int W = kWaves>
 __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__restrict__ wx,
                                                int G32, int xbytes, float xinv, int wave, int lane,
-                                               const float *bias, f32x16 (&acc)[MR][NR]) {
+                                               const float *bias, f32x16 (&acc)[MR][NR],
+                                               unsigned long long *st_first = nullptr) {
   const _Float16 *ap = hplane(const_cast<float *>(H), lane & 15) + 8 * (lane >> 4);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
   WStepH16<NR> w[kH16Ring];
@@ -815,6 +816,7 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
     static_for<kH16Ring>([&](auto u) {
       step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
                                 g + u.value, c4);
+      if (u.value == 0 && g == 0) stamp(st_first);  // diagnostic: first K step done
     });
   }
   const _Float16 *ab = ap + 32 * g;
@@ -1057,7 +1059,7 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
     }
     else if constexpr (kH16)  // G16: 32-deep K steps here
       layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
-                                xinv, wave, lane, bias, acc);
+                                xinv, wave, lane, bias, acc, st_first);
     else
       layer_gemm_h<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024,
                               xinv, wave, lane, bias, acc);
