@@ -117,7 +117,7 @@ def test_gather_layout():
     assert L.nregion == 1 and L.row_bytes[0] == 16 and L.block_bytes == 125_000 * 16 + 64
 
 
-@pytest.mark.parametrize("world,n", [(2, 1001), (2, 64), (3, 1000)])
+@pytest.mark.parametrize("world,n", [(2, 1001), (2, 64), (3, 1000), (2, 1), (3, 2)])
 def test_gather_matches_single_process(world, n):
     from inversekinematicsann_amd.robot.position_generator import random_dist
     pts = random_dist(n, seed=11)
