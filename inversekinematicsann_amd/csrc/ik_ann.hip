@@ -1159,6 +1159,9 @@ constexpr int ann_waves() {
                                          : kWaves;
 }
 
+#ifndef IKHIP_ANN_DYN  // 1: tiles claimed from a counter after the first; 0: static stride
+#define IKHIP_ANN_DYN 1
+#endif
 template <int MR, int X>
 __global__ __launch_bounds__((64 * ann_waves<MR, X>()), (MR == 2 || kWide) ? 1 : 2) void
 ann_fused_kernel(AnnArgs a) {
@@ -1171,12 +1174,26 @@ ann_fused_kernel(AnnArgs a) {
   const int64_t ntiles = (a.n + BM - 1) / BM;
   double blk_max = 0.0, blk_sum = 0.0;  // FK round-trip error of this lane's points
 
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+#if IKHIP_ANN_DYN
+  // tiles after the first are claimed from a launch-wide counter (DevStats heads[0],
+  // zeroed by the stats reset before every solve): a workgroup that runs faster
+  // (an XCD at a higher clock, a CU whose partner workgroup has finished) takes more
+  // tiles, so the launch does not end on the slowest workgroup's static share.  The
+  // claim is issued at a tile's start and read after its last barrier; two slots,
+  // so thread 0's next claim never overwrites the one the others are still reading.
+  __shared__ long long next_tile[2];
+  unsigned long long *const tile_ctr = &a.S->heads[0][0];
+#endif
+  int64_t it_local = 0;  // this workgroup's tile counter
+  for (int64_t tile = blockIdx.x; tile < ntiles; ++it_local) {
+#if IKHIP_ANN_DYN
+    if (tid == 0)
+      next_tile[it_local & 1] = (long long)atomicAdd(tile_ctr, 1ull) + (long long)gridDim.x;
+#endif
     const int64_t pt = tile * BM + tid;
     // diagnostic stamps (block 0, first tiles, lane 0 of each wave): slot 0 tile
     // start, 1 staged, 2+2l layer l GEMM done, 3+2l layer l done, 31 tile done
     unsigned long long *stp = nullptr;
-    const int64_t it_local = tile / gridDim.x;  // this workgroup's tile counter
     if (a.dbg && blockIdx.x == 0 && lane == 0 && it_local < kStampTiles && wave < kWaves)
       stp = a.dbg + ((size_t)it_local * kWaves + wave) * kStampSlots;
     stamp(stp);
@@ -1283,6 +1300,11 @@ ann_fused_kernel(AnnArgs a) {
     }
     __syncthreads();  // the next tile's staging overwrites H
     stamp(stp ? stp + kStampSlots - 1 : nullptr);
+#if IKHIP_ANN_DYN
+    tile = (int64_t)next_tile[it_local & 1];
+#else
+    tile += gridDim.x;
+#endif
   }
   // per-block FK-error stats: one atomic pair per wave holding points, into its shard.
   // The whole wave reduces (lanes >= BM hold zeros): at MR = 1 the upper half of
