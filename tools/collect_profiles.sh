@@ -2,12 +2,13 @@
 # profiles/<round>/ (gpurun_out/ is scratch): rocprofv3 --stats kernel tables,
 # per-kernel FETCH_SIZE / WRITE_SIZE summaries, the bench line, traffic.json.
 #   bash tools/collect_profiles.sh r01
+#   MODES="ann ann_fp16x3" bash tools/collect_profiles.sh r02   # the modes a run re-profiled
 set -e
 R=${1:?round name}
 OUT=gpurun_out
 DST=profiles/$R
 mkdir -p $DST/pmc
-for m in ann fabrik ann_bf16x6 ann_fp16x3 fk; do
+for m in ${MODES:-ann fabrik ann_bf16x6 ann_fp16x3 fk}; do
   # gpurun_out/ accumulates the runs of earlier calls: take the newest
   cp "$(ls -t $OUT/prof_stats_$m/*/*_kernel_stats.csv | head -1)" $DST/${m}_kernel_stats.csv
   for c in fetch write; do
