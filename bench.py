@@ -10,12 +10,16 @@ inputs already resident in HBM.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--method ann|fabrik]
                     [--total-points T] [--gather 0|1]
 
-N > 1 is launched one process per GPU (torch.distributed.run).  Every rank
-holds the same global batch (random_dist, seed 0; seed 1 from 10M points) and
-calls the library's sharded solve (ik_*_solve_sharded): it solves its
-contiguous shard and ONE RCCL all-gather inside libikhip delivers every
-rank's rows plus a tail record of its stats, so the step ends
-with the whole batch on every rank.  Weak scaling by default (1M points per
+N > 1 runs one process per GPU: `python bench.py --gpus N` starts
+`python -m torch.distributed.run --nproc-per-node N bench.py ...` itself as a
+child process (before anything here touches the GPU) and exits with its code;
+a rank that finds WORLD_SIZE != --gpus exits non-zero instead of printing a
+mislabeled line.  Every rank holds the same global batch (random_dist, seed 0;
+seed 1 from 10M points) and calls the library's sharded solve
+(ik_*_solve_sharded): it solves its parts of the batch and the library
+all-gathers them in place over RCCL, chunk by chunk under the solve, with a
+tail record of every rank's stats, so the step ends with the
+whole batch's angles on every rank.  Weak scaling by default (1M points per
 GPU); --total-points 10000000 is configs[3] (ANN) / configs[4] (FABRIK tol
 1e-5 / 200) as strong scaling.  torch.distributed (gloo) is only the control
 plane: the RCCL id exchange, the barriers, the max over ranks of the step time.
@@ -44,6 +48,45 @@ SPLIT_PRODUCTS = {"bf16x6": 6, "fp16x3": 3}  # MFMA products per fp32 product
 FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
 HBM_PEAK = 8.0e12           # bytes/s
 FABRIK_FLOP_PER_ITER = 132
+
+
+def launch_command(argv, gpus, port):
+    """The torch.distributed.run command line that runs this script on `gpus`
+    ranks of one node (the driver's N > 1 form, BASELINE.json / SURVEY 8(e))."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr", "127.0.0.1",
+            f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def _gpus_arg(argv):
+    for i, a in enumerate(argv):
+        if a == "--gpus" and i + 1 < len(argv):
+            return int(argv[i + 1])
+        if a.startswith("--gpus="):
+            return int(a.split("=", 1)[1])
+    return 1
+
+
+def maybe_launch(argv=None):
+    """`--gpus N > 1` without a launcher: run N ranks as a child torch.distributed.run
+    (rank 0 prints the line on the inherited stdout) and return its exit code;
+    None when this process is a rank itself (or N == 1).  Nothing here imports
+    torch or touches the GPU: the child is a new program, not an exec."""
+    argv = sys.argv[1:] if argv is None else argv
+    if "WORLD_SIZE" in os.environ:
+        return None
+    gpus = _gpus_arg(argv)
+    if gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launch_command(argv, gpus, port), env=env)
 
 
 def parse():
@@ -198,7 +241,23 @@ def _stats_over_ranks(job, st, res):
             sum_over_ranks(st.sum_iters, w), sum_over_ranks(st.n_capped, w))
 
 
-def _p99(derr, world):
+def _own_parts(job):
+    """This rank's rows [(begin, end)] of the last step: its parts of the chunks
+    the library planned the sharded call with (ik_comm_info), else its shard."""
+    if job.sc is None:
+        return [(0, job.n_local)]
+    from inversekinematicsann_amd import dist as D
+    _, _, chunks = job.sc.info()
+    C, _, _ = D.plan_of(job.total, job.world, max(1, chunks))
+    return [D.part_bounds(job.total, job.world, max(1, chunks), job.sc.rank, c) for c in range(C)]
+
+
+def _p99(job, derr, world):
+    """p99 of the FK errors: after a sharded step the library's gathered
+    histograms (every rank's own rows; an upper bound within 1/16 octave), else
+    torch.quantile of this rank's errors, max over ranks."""
+    if job.sc is not None:
+        return job.sc.fk_err_quantile(0.99)
     import torch
     fin = derr[:1 << 24]
     fin = fin[torch.isfinite(fin)]
@@ -266,10 +325,13 @@ def run_ann(job, args, mode="fp32"):
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
+    if job.sc is not None:
+        res["gather_chunks"] = job.sc.info()[2]
+        res["gather_ms"] = st.gather_ms
     mx, sm, _, _ = _stats_over_ranks(job, st, res)
     res["max_fk_err"] = mx
     res["mean_fk_err"] = sm / job.total
-    res["p99_fk_err"] = _p99(derr, world)
+    res["p99_fk_err"] = _p99(job, derr, world)
     res["fk_err_note"] = ("random Glorot weights (the reference .h5 is not shipped): the FK "
                           "round trip is computed in the same launch; not model accuracy")
     res["outputs"] = {"ang": dang}
@@ -332,20 +394,22 @@ def run_fabrik(job, args, tol=None, max_iter=None):
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
+    if job.sc is not None:
+        res["gather_chunks"] = job.sc.info()[2]
+        res["gather_ms"] = st.gather_ms
     mx, sm, sum_iters, n_capped = _stats_over_ranks(job, st, res)
     n = job.n_local
     res["mean_iters"] = sum_iters / job.total
     res["n_capped"] = int(n_capped)
     res["max_fk_err"] = mx
     res["mean_fk_err"] = sm / job.total
-    res["p99_fk_err"] = _p99(derr, world)
+    res["p99_fk_err"] = _p99(job, derr, world)
     res["outputs"] = {"ang": dang, "iters": dit}
     if args.end_to_end:
         res["end_to_end"] = end_to_end(
             job, lambda hp, pinned: _host_fabrik(job, hp, pinned, tol, max_iter), args)
     # this rank's own iterations (the kernel's work), from its shard of the rows
-    own = dit[job.lo:job.hi] if job.sc is not None else dit
-    local_iters = int(own.sum().item())
+    local_iters = sum(int(dit[b:e].sum().item()) for b, e in _own_parts(job))
     k = res["kernels"].get("fabrik_iter_kernel")
     flops = FABRIK_FLOP_PER_ITER * local_iters
     achieved = flops / (k / 1e3) if k else None
@@ -616,10 +680,21 @@ def _config_ref(method, total, world, tol, max_iter):
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # a line labelled with one GPU count must measure that many ranks
+        print(f"bench.py: --gpus {args.gpus} but {world} rank(s) (WORLD_SIZE); launch N > 1 "
+              f"as `python bench.py --gpus N` (it starts the ranks itself) or with "
+              f"torch.distributed.run --nproc-per-node N", file=sys.stderr)
+        sys.exit(2)
     import torch
+    if os.environ.get("IKHIP_DIST_BACKEND", "rccl") != "gloo" and \
+            torch.cuda.device_count() < world:
+        print(f"bench.py: {world} ranks but {torch.cuda.device_count()} GPU(s) visible "
+              "(one rank per GPU; IKHIP_DIST_BACKEND=gloo --gather 0 rehearses more ranks "
+              "than GPUs)", file=sys.stderr)
+        sys.exit(2)
     world, rank, local = dist_setup(args)
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     from inversekinematicsann_amd import _native
     from inversekinematicsann_amd import dist as D
     from inversekinematicsann_amd.robot.position_generator import random_dist
@@ -661,7 +736,8 @@ def main():
                                 "roofline": r2["roofline"], "workload": r2["workload"],
                                 "kernels_ms": r2["kernels"],
                                 **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
-                                                      "mean_iters", "n_capped", "end_to_end")
+                                                      "mean_iters", "n_capped", "end_to_end",
+                                                      "gather_chunks", "gather_ms")
                                    if k in r2}}
             cref = _config_ref("fabrik" if other.startswith("fabrik") else other, total, world,
                                1e-5 if other == "fabrik_tol1e-5" else args.tol,
@@ -686,9 +762,13 @@ def main():
                    "parallelism": f"dp{world}", "method": args.method,
                    "ann_mode": args.ann_mode if args.method == "ann" else None,
                    "all_gather_in_step": sc is not None,
-                   "collective": ("one RCCL all-gather per step inside libikhip "
-                                  "(ik_*_solve_sharded): rows + per-rank stats tail")
+                   "collective": ("RCCL all-gathers inside libikhip (ik_*_solve_sharded): each "
+                                  "chunk's angles (+ FABRIK iterations) gathered in place under "
+                                  "the next chunk's solve; per-rank stats tail + FK-error "
+                                  "histogram with the last chunk; FK errors stay local")
                    if sc is not None else None,
+                   "n_ranks_rccl": sc.info()[0] if sc is not None else None,
+                   "gather_chunks": res.get("gather_chunks"),
                    "tol": args.tol if args.method == "fabrik" else None,
                    "max_iter": args.max_iter if args.method == "fabrik" else None},
         "roofline": res["roofline"],
@@ -696,7 +776,7 @@ def main():
         "kernels_ms": res["kernels"],
     }
     for k in ("max_fk_err", "mean_fk_err", "p99_fk_err", "fk_err_note", "mean_iters", "n_capped",
-              "end_to_end"):
+              "end_to_end", "gather_ms"):
         if k in res:
             line[k] = res[k]
     if secondary:
@@ -734,4 +814,7 @@ def main():
 
 
 if __name__ == "__main__":
+    rc = maybe_launch()
+    if rc is not None:
+        sys.exit(rc)
     main()

@@ -69,7 +69,11 @@ typedef struct ik_stats {
 int ik_ctx_create(int device, ik_ctx **out);
 int ik_ctx_destroy(ik_ctx *ctx);
 /* Use an external stream (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+ * NULL restores the context's own stream.  A context's device work is one
+ * sequence whatever the streams: a call enqueued on another stream than the
+ * previous call first waits (hipStreamWaitEvent) for the previous call's work,
+ * so two calls never share the context's stats / work-queue words at once.
+ * Host threads must still not call into one context concurrently. */
 int ik_ctx_set_stream(ik_ctx *ctx, void *stream);
 void *ik_ctx_get_stream(ik_ctx *ctx);
 const char *ik_last_error(void); /* thread-local message of the last failure */
@@ -93,7 +97,7 @@ int ik_check_limits(ik_ctx *ctx, const double *pts, int64_t n, int flags, ik_sta
 int ik_fk(ik_ctx *ctx, const double *ang, int64_t n, double *xyz, double *mats, int flags,
           ik_stats *stats);
 
-/* ForwardKinematics(dh).fkine for a DH table of nj (2..8) joints (the reference
+/* ForwardKinematics(dh).fkine for a DH table of nj (2..1024) joints (the reference
  * takes any nj >= 3, forward.py:13-19): dh host 4 x nj row-major (thetas, d, a,
  * alpha), ang n x nj -> effector xyz n x 3 and, if mats is not NULL, the nj
  * cumulative 4 x 4 transforms (n x nj x 16; the reference's nj x nj matrices
@@ -192,15 +196,27 @@ int ik_stats_fetch(ik_ctx *ctx, ik_stats *stats);
  * The reference scales by competing consumers of one RabbitMQ queue
  * (rpc_broker.py:55-68); here one process per GPU shares the batch instead.
  * Every rank calls the sharded solve with the same whole batch (n points, host
- * or device pointer); rank r solves rows [floor(r n / g), floor((r+1) n / g))
- * (ik_shard_range) and ONE all-gather over RCCL delivers every rank's rows and a
- * tail record of its batch stats (ik_shard_tail), so each rank returns the whole
- * batch's angles and the whole batch's stats (first_oob / first_err are the
- * lowest GLOBAL indices: the reference's sequential exception precedence).
- * With a device pointer only the rank's own rows of pts are read.  RCCL is
- * loaded at ik_comm_init (the process's librccl if already loaded -- torch
- * ships one --, else librccl.so.1; IKHIP_RCCL_LIB overrides). */
+ * or device pointer).  The batch is cut into C chunks of g parts each
+ * (ik_shard_plan): rank r solves part (c, r) = rows [(c g + r) S, (c g + r + 1) S)
+ * of every chunk c (S = ceil(n / (C g)), clipped to n), writing the results at
+ * their global rows of the caller's arrays, and chunk c's rows are all-gathered
+ * IN PLACE (ncclAllGather with sendbuf = recvbuf + r S rows) while chunk c + 1 is
+ * solved: no pack, no unpack, no padding except in the one ragged last chunk
+ * (gathered through a staging buffer and copied out).  Gathered per row: the
+ * angles and, for FABRIK, the iteration counts.  The per-point FK error stays
+ * local: only the rank's own rows of fk_err are written; the batch's FK-error
+ * max / sum / quantiles come from a 64-byte tail record (ik_shard_tail) and a
+ * histogram that ride with the last chunk's all-gather, as do first_oob /
+ * first_err (the lowest GLOBAL indices: the reference's sequential exception
+ * precedence).  With a device pointer only the rank's own rows of pts are read.
+ * RCCL is loaded at ik_comm_init (the process's librccl if already loaded --
+ * torch ships one --, else librccl.so.1; IKHIP_RCCL_LIB overrides). */
 #define IK_COMM_ID_BYTES 128
+#define IK_MAX_GATHER_CHUNKS 8
+/* FK-error histogram of a rank (uint32 counts, gathered with the tail): finite
+ * e >= 0 falls in bin 16 (E - 959) + m, E the biased float64 exponent and m the top
+ * 4 mantissa bits, clamped to [0, 2047] (2^-64 .. 2^64, 1/16 octave per bin). */
+#define IK_FKHIST_BINS 2048
 
 /* The stats of one rank's shard as gathered (64 bytes). */
 typedef struct ik_shard_tail {
@@ -211,17 +227,14 @@ typedef struct ik_shard_tail {
   int64_t rows; /* rows the rank solved */
 } ik_shard_tail;
 
-/* The per-rank block of the all-gather, bytes: the rank's rows of each output
- * region (angles, then iterations / FK errors when gathered), padded to the
- * largest shard, then the tail record. */
-typedef struct ik_gather_layout {
-  int64_t shard;        /* rows per block (the largest shard) */
-  int64_t block_bytes;  /* bytes per rank */
-  int32_t nregion;      /* 1..3 */
-  int32_t row_bytes[3]; /* bytes per row of each region */
-  int64_t offset[3];    /* byte offset of each region in the block */
-  int64_t tail_offset;  /* byte offset of the ik_shard_tail */
-} ik_gather_layout;
+/* How a batch of n rows is split over nranks ranks in chunks (host only). */
+typedef struct ik_shard_plan {
+  int64_t n;         /* rows of the batch */
+  int32_t nranks;    /* g */
+  int32_t chunks;    /* C: chunks that hold rows (<= the requested count) */
+  int64_t part_rows; /* S: rows of one rank's part of one chunk */
+  int64_t full_rows; /* rows of the chunks gathered in place (the rest is staged) */
+} ik_shard_plan;
 
 enum { IK_METHOD_ANN = 0, IK_METHOD_FABRIK = 1 };
 
@@ -231,18 +244,39 @@ int ik_comm_unique_id(uint8_t *id /* IK_COMM_ID_BYTES */);
  * communicator (one GPU per rank). */
 int ik_comm_init(ik_ctx *ctx, int nranks, int rank, const uint8_t *id);
 int ik_comm_destroy(ik_ctx *ctx);
+/* The communicator as the library holds it: ranks, this rank, and the chunk
+ * count the last sharded call was planned with (ik_shard_plan_of's chunks; 0
+ * before one), so a caller can find its own rows with ik_shard_part. */
+int ik_comm_info(ik_ctx *ctx, int *nranks, int *rank, int *last_chunks);
+/* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic: FABRIK
+ * 4 when a rank's share is >= 256k rows, else 1; ANN 1 (its gather is ~1 % of
+ * its solve).  Environment default: IKHIP_GATHER_CHUNKS. */
+int ik_comm_set_chunks(ik_ctx *ctx, int chunks);
 /* Host-only helpers of the protocol (no device needed). */
+int ik_shard_plan_of(int64_t n, int nranks, int chunks, ik_shard_plan *out);
+/* Rank's part of chunk c: rows [begin, end) (empty when begin == end). */
+int ik_shard_part(const ik_shard_plan *plan, int rank, int chunk, int64_t *begin, int64_t *end);
+/* = ik_shard_part of the one-chunk plan: rank's rows [r S, (r + 1) S) clipped, S = ceil(n / g). */
 int ik_shard_range(int64_t n, int nranks, int rank, int64_t *begin, int64_t *end);
-int ik_gather_layout_of(int method, int64_t n, int nranks, int with_iters, int with_fk_err,
-                        ik_gather_layout *out);
 int ik_tail_reduce(const ik_shard_tail *tails, int nranks, ik_stats *out);
+/* The bin of an FK error (see IK_FKHIST_BINS; -1 for NaN / inf / negative) and
+ * the upper edge of a bin. */
+int ik_fkhist_bin(double e);
+double ik_fkhist_upper(int bin);
+/* q-quantile (0 < q <= 1) of the FK errors of the last sharded call, from the
+ * gathered histograms: the upper edge of the bin holding the ceil(q m)-th
+ * smallest of the m finite errors (an upper bound, within 1/16 octave).  Needs
+ * fk_err in that call; waits for it. */
+int ik_fk_err_quantile(ik_ctx *ctx, double q, double *out);
 
 /* AnnInverseKinematics.ikine / ANN.predict (see ik_ann_solve) over the ranks:
- * ang n x 4 float32 and fk_err (nullable) n float64 of the WHOLE batch. */
+ * ang n x 4 float32 of the WHOLE batch; fk_err (nullable) n float64, of which
+ * only this rank's rows are written. */
 int ik_ann_solve_sharded(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *fk_err,
                          int flags, ik_stats *stats);
 /* FabrikInverseKinematics.ikine (see ik_fabrik_solve_fk) over the ranks: ang n x 4
- * float64, iters (nullable) n int32, fk_err (nullable) n float64, whole batch. */
+ * float64 and iters (nullable) n int32 of the whole batch, fk_err (nullable) n
+ * float64 of this rank's rows. */
 int ik_fabrik_solve_sharded(ik_ctx *ctx, const double *pts, int64_t n, double tol,
                             int32_t max_iter, double *ang, int32_t *iters, double *fk_err,
                             int flags, ik_stats *stats);

@@ -25,6 +25,8 @@ IK_OK, IK_E_OUT_OF_REACH, IK_E_DOMAIN, IK_E_ZERODIV, IK_E_ANGLE_RANGE = 0, 1, 2,
 IK_E_BADARG, IK_E_HIP, IK_E_NOMODEL, IK_E_RCCL = 16, 17, 18, 19
 IK_METHOD_ANN, IK_METHOD_FABRIK = 0, 1
 IK_COMM_ID_BYTES = 128
+IK_MAX_GATHER_CHUNKS = 8
+IK_FKHIST_BINS = 2048
 IK_F_DEVICE, IK_F_ASYNC, IK_F_NO_LIMITS = 1, 2, 4
 ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
 
@@ -33,9 +35,11 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode",
-                    "ik_comm_unique_id", "ik_comm_init", "ik_comm_destroy", "ik_shard_range",
-                    "ik_gather_layout_of", "ik_tail_reduce", "ik_ann_solve_sharded",
-                    "ik_fabrik_solve_sharded", "ik_host_alloc", "ik_host_free")
+                    "ik_comm_unique_id", "ik_comm_init", "ik_comm_destroy", "ik_comm_info",
+                    "ik_comm_set_chunks", "ik_shard_plan_of", "ik_shard_part", "ik_shard_range",
+                    "ik_tail_reduce", "ik_fkhist_bin", "ik_fkhist_upper", "ik_fk_err_quantile",
+                    "ik_ann_solve_sharded", "ik_fabrik_solve_sharded", "ik_host_alloc",
+                    "ik_host_free")
 ANN_MODES = {"fp32": 0, "bf16x6": 1, "fp16x3": 2}
 
 
@@ -69,11 +73,10 @@ class ShardTail(ctypes.Structure):
                 ("rows", ctypes.c_int64)]
 
 
-class GatherLayout(ctypes.Structure):
-    """ik_gather_layout: the per-rank block of the sharded solves' all-gather."""
-    _fields_ = [("shard", ctypes.c_int64), ("block_bytes", ctypes.c_int64),
-                ("nregion", ctypes.c_int32), ("row_bytes", ctypes.c_int32 * 3),
-                ("offset", ctypes.c_int64 * 3), ("tail_offset", ctypes.c_int64)]
+class ShardPlan(ctypes.Structure):
+    """ik_shard_plan: a batch split over the ranks in chunks (include/ikhip.h)."""
+    _fields_ = [("n", ctypes.c_int64), ("nranks", ctypes.c_int32), ("chunks", ctypes.c_int32),
+                ("part_rows", ctypes.c_int64), ("full_rows", ctypes.c_int64)]
 
 
 _lib = None
@@ -132,11 +135,19 @@ def load_library(path: str = LIB_PATH):
         L.ik_comm_unique_id.argtypes = [vp]
         L.ik_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
         L.ik_comm_destroy.argtypes = [vp]
+        ipt = ctypes.POINTER(ctypes.c_int)
+        L.ik_comm_info.argtypes = [vp, ipt, ipt, ipt]
+        L.ik_comm_set_chunks.argtypes = [vp, ctypes.c_int]
+        L.ik_shard_plan_of.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ShardPlan)]
+        L.ik_shard_part.argtypes = [ctypes.POINTER(ShardPlan), ctypes.c_int, ctypes.c_int,
+                                    ctypes.POINTER(i64), ctypes.POINTER(i64)]
         L.ik_shard_range.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64),
                                      ctypes.POINTER(i64)]
-        L.ik_gather_layout_of.argtypes = [ctypes.c_int, i64, ctypes.c_int, ctypes.c_int,
-                                          ctypes.c_int, ctypes.POINTER(GatherLayout)]
         L.ik_tail_reduce.argtypes = [vp, ctypes.c_int, st]
+        L.ik_fkhist_bin.argtypes = [ctypes.c_double]
+        L.ik_fkhist_upper.argtypes = [ctypes.c_int]
+        L.ik_fkhist_upper.restype = ctypes.c_double
+        L.ik_fk_err_quantile.argtypes = [vp, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
         L.ik_ann_solve_sharded.argtypes = [vp, dp, i64, dp, dp, ctypes.c_int, st]
         L.ik_fabrik_solve_sharded.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp,
                                               ctypes.c_int, st]
@@ -418,6 +429,24 @@ class Context:
     def comm_destroy(self):
         self._check(self.lib.ik_comm_destroy(self.handle))
 
+    def comm_info(self):
+        """(ranks of the library's communicator, this rank, chunks of the last sharded call)."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._check(self.lib.ik_comm_info(self.handle, ctypes.byref(a), ctypes.byref(b),
+                                          ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+    def comm_set_chunks(self, chunks: int):
+        """Chunks of the sharded solves' in-place all-gathers (0 = automatic)."""
+        self._check(self.lib.ik_comm_set_chunks(self.handle, int(chunks)))
+
+    def fk_err_quantile(self, q: float) -> float:
+        """q-quantile (upper bound, 1/16 octave) of the last sharded call's FK errors,
+        from every rank's gathered histogram."""
+        out = ctypes.c_double()
+        self._check(self.lib.ik_fk_err_quantile(self.handle, float(q), ctypes.byref(out)))
+        return out.value
+
     def ann_solve_sharded(self, pts, check_limits=True, want_fk_err=False):
         """Host arrays: every rank passes the whole batch and gets the whole batch's
         angles (float32) and stats back; it solves only its own shard."""
@@ -556,14 +585,30 @@ def shard_range(n: int, nranks: int, rank: int):
     return b.value, e.value
 
 
-def gather_layout(method: int, n: int, nranks: int, with_iters: bool = False,
-                  with_fk_err: bool = False) -> GatherLayout:
-    """ik_gather_layout_of (host only): the per-rank block of the all-gather."""
-    L = GatherLayout()
-    _host_check(load_library().ik_gather_layout_of(int(method), int(n), int(nranks),
-                                                   int(bool(with_iters)), int(bool(with_fk_err)),
-                                                   ctypes.byref(L)))
-    return L
+def shard_plan(n: int, nranks: int, chunks: int = 1) -> ShardPlan:
+    """ik_shard_plan_of (host only): the batch in chunks of nranks parts."""
+    p = ShardPlan()
+    _host_check(load_library().ik_shard_plan_of(int(n), int(nranks), int(chunks),
+                                                ctypes.byref(p)))
+    return p
+
+
+def shard_part(plan: ShardPlan, rank: int, chunk: int):
+    """ik_shard_part (host only): rank's rows [begin, end) of the chunk."""
+    b, e = ctypes.c_int64(), ctypes.c_int64()
+    _host_check(load_library().ik_shard_part(ctypes.byref(plan), int(rank), int(chunk),
+                                             ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
+def fkhist_bin(e: float) -> int:
+    """ik_fkhist_bin: the FK-error histogram bin of e (-1: not counted)."""
+    return int(load_library().ik_fkhist_bin(float(e)))
+
+
+def fkhist_upper(b: int) -> float:
+    """ik_fkhist_upper: the upper edge of histogram bin b."""
+    return float(load_library().ik_fkhist_upper(int(b)))
 
 
 def tail_reduce(tails: Sequence[ShardTail]) -> IkStats:

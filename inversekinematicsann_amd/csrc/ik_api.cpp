@@ -52,12 +52,21 @@ int fail(int code, const std::string &msg) {
   return code;
 }
 
-KtScope::KtScope(ik_ctx *c) {
+KtScope::KtScope(ik_ctx *c) : c_(c) {
   g_kt = &c->kt;
   c->kt.n = 0;
+  // calls on one context share its stats block and work-queue words: a call on
+  // another stream than the last one starts after that one's work
+  if (c->call_done_set && c->last_stream && c->last_stream != c->stream)
+    (void)hipStreamWaitEvent(c->stream, c->call_done, 0);
   c->last_stream = c->stream;  // every enqueueing entry point opens one
+  c->last_piped = false;
 }
-KtScope::~KtScope() { g_kt = nullptr; }
+KtScope::~KtScope() {
+  g_kt = nullptr;
+  if (c_->call_done && hipEventRecord(c_->call_done, c_->stream) == hipSuccess)
+    c_->call_done_set = true;
+}
 
 int ensure_scratch(ik_ctx *c, size_t bytes) {
   if (bytes <= c->scratch_bytes) return IK_OK;
@@ -170,6 +179,7 @@ int ik_ctx_create(int device, ik_ctx **out) {
   if (e == hipSuccess) e = hipMalloc(&c->fab_ord, sizeof(FabOrderDev));
   if (e == hipSuccess) e = hipMemset(c->fab_ord, 0, sizeof(FabOrderDev));
   if (e == hipSuccess) e = hipMalloc(&c->rconst, sizeof(RobotConstDev));
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->call_done, hipEventDisableTiming);
   c->stream = c->own_stream;
   if (e != hipSuccess) {
     (void)ik_ctx_destroy(c);  // frees whatever was allocated
@@ -209,6 +219,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   comm_release(c);
   pipe_release(c);
+  if (c->call_done) (void)hipEventDestroy(c->call_done);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   for (int i = 0; i < kMaxTimed; ++i) {
     if (c->kt.beg[i]) (void)hipEventDestroy(c->kt.beg[i]);
@@ -323,6 +334,10 @@ int ik_stats_fetch(ik_ctx *c, ik_stats *stats) {
   if (rc) return rc;
   // the stats of the last call live on the stream it ran on (ik_ctx_set_stream may
   // have switched since)
+  if (c->last_piped) {  // a chunked host pipeline: merged when it returned
+    if (stats) *stats = c->piped_stats;
+    return IK_OK;
+  }
   hipStream_t cur = c->stream;
   if (c->last_stream) c->stream = c->last_stream;
   rc = c->last_sharded ? sharded_stats(c, stats) : finish(c, 0, stats);
@@ -383,8 +398,9 @@ int ik_fk(ik_ctx *c, const double *ang, int64_t n, double *xyz, double *mats, in
 
 int ik_fk_chain(ik_ctx *c, int nj, const double *dh, const double *ang, int64_t n,
                 double *xyz, double *mats, int flags, ik_stats *stats) {
-  if (!c || nj < 2 || nj > 8 || !dh || n < 0 || (n > 0 && (!ang || !xyz)))
-    return fail(IK_E_BADARG, "ik_fk_chain: bad args (nj must be 2..8)");
+  if (!c || nj < 2 || nj > kFkMaxJoints || !dh || n < 0 || (n > 0 && (!ang || !xyz)))
+    return fail(IK_E_BADARG, "ik_fk_chain: bad args (nj must be 2.." +
+                                 std::to_string(kFkMaxJoints) + ")");
   if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
     return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
   int rc = set_dev(c);

@@ -54,6 +54,18 @@ struct d3 {
   double x, y, z;
 };
 
+// The FK-error histogram bin of e (ikhip.h IK_FKHIST_BINS): 16 bins per octave
+// from the float64 exponent and top 4 mantissa bits, monotonic in e; -1 for NaN,
+// inf and negative values (not counted, like the max / sum stats).
+__host__ __device__ inline int fkhist_bin(double e) {
+  if (!(e >= 0.0) || e > 1.7976931348623157e308) return -1;
+  uint64_t b;
+  __builtin_memcpy(&b, &e, sizeof(b));
+  b &= 0x7fffffffffffffffull;
+  const int k = ((int)(b >> 52) - (1023 - 64)) * 16 + (int)((b >> 48) & 15);
+  return k < 0 ? 0 : (k >= IK_FKHIST_BINS ? IK_FKHIST_BINS - 1 : k);
+}
+
 // The reference's pow(v, 2).
 __device__ __forceinline__ double sq(double v) { return v * v; }
 
@@ -492,7 +504,9 @@ void launch_check_limits(const RobotDev &r, const double *pts, int64_t n, DevSta
                          hipStream_t st);
 void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, double *mats,
                DevStats *S, hipStream_t st);
-// FK of a chain of nj (2..8) joints; dh: device 4 x nj, mats nullable n x nj x 16.
+// FK of a chain of nj (2..kFkMaxJoints) joints; dh: device 4 x nj, mats nullable
+// n x nj x 16 (2..8 unrolled, longer chains a run-time joint loop).
+constexpr int kFkMaxJoints = 1024;
 void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double *xyz,
                  double *mats, DevStats *S, hipStream_t st);
 // FABRIK work order (ik_fabrik.hip "Work order"): per context, the largest

@@ -201,6 +201,37 @@ __global__ __launch_bounds__(256) void fk_n_kernel(const double *__restrict__ dh
   xyz[3 * i + 2] = e.z;
 }
 
+// The same chain for any number of joints (longer than the unrolled builds
+// above): the joint loop runs at run time, the arithmetic is fk_n_kernel's.
+__global__ __launch_bounds__(256) void fk_any_kernel(int nj, const double *__restrict__ dh,
+                                                     const double *__restrict__ ang, int64_t n,
+                                                     double *__restrict__ xyz,
+                                                     double *__restrict__ mats, DevStats *S) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int st = IK_OK;
+  double M[16], A[16];
+  for (int k = 0; k < nj; ++k) {
+    const double th = ang[(size_t)i * nj + k];
+    if (!angle_ok(th) || !angle_ok(dh[3 * nj + k])) st = IK_E_ANGLE_RANGE;
+    dh_transform(th, dh[nj + k], dh[2 * nj + k], dh[3 * nj + k], k == 0 ? M : A);
+    if (k > 0) mm4(M, A, M);
+    if (mats) {
+      double *o = mats + ((size_t)i * nj + k) * 16;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[e] = M[e];
+    }
+  }
+  d3 e = {M[3], M[7], M[11]};
+  if (st != IK_OK) {
+    record_error(S, i, st);
+    e.x = e.y = e.z = __builtin_nan("");
+  }
+  xyz[3 * i] = e.x;
+  xyz[3 * i + 1] = e.y;
+  xyz[3 * i + 2] = e.z;
+}
+
 void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double *xyz,
                  double *mats, DevStats *S, hipStream_t st) {
   if (n <= 0) return;
@@ -219,6 +250,7 @@ void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double 
     IK_FKN(7)
     IK_FKN(8)
     default:
+      hipLaunchKernelGGL(fk_any_kernel, dim3(grid), dim3(256), 0, st, nj, dh, ang, n, xyz, mats, S);
       break;
   }
 #undef IK_FKN

@@ -22,16 +22,33 @@ struct KTimer {
 };
 }  // namespace ikhip
 
-// One RCCL communicator of a context (ik_comm_init): the buffers of the one
-// all-gather per sharded solve, grow-only like the scratch.
+// One rank's tail block as gathered: the stats record, then its FK-error histogram.
+struct IkTailBlock {
+  ik_shard_tail t;
+  uint32_t hist[IK_FKHIST_BINS];
+};
+
+// One RCCL communicator of a context (ik_comm_init) and the state of the
+// chunked in-place all-gathers of the sharded solves (ik_shard.hip), grow-only
+// like the scratch.
 struct IkComm {
   void *comm = nullptr;  // ncclComm_t
   int nranks = 0, rank = -1;
-  void *send = nullptr, *recv = nullptr;  // device: this rank's block, all blocks
-  size_t send_bytes = 0, recv_bytes = 0;
-  ik_shard_tail *h_tails = nullptr;  // pinned: every rank's tail record
-  int h_tails_n = 0;
-  hipEvent_t g0 = nullptr, g1 = nullptr;  // around the all-gather
+  int chunks_req = 0;    // ik_comm_set_chunks (0 = automatic)
+  int last_chunks = 0;   // all-gathers of the last sharded call (its plan's chunks)
+  int last_req = 0;      // the chunk count that plan was made with (ik_comm_info)
+  bool last_hist = false;  // the last sharded call gathered FK-error histograms
+  hipStream_t cs = nullptr;  // the gathers' stream
+  void *stage = nullptr;     // the ragged last chunk's rows (all regions)
+  size_t stage_bytes = 0;
+  IkTailBlock *tail_send = nullptr;  // device: this rank's tail block
+  IkTailBlock *tail_recv = nullptr;  // device: every rank's
+  IkTailBlock *h_tails = nullptr;    // pinned: every rank's
+  int tails_n = 0;
+  ikhip::DevStats *d_cstats = nullptr;  // one stats block per chunk
+  hipEvent_t ev_solved[IK_MAX_GATHER_CHUNKS] = {};  // chunk k's rows written (solve stream)
+  hipEvent_t ev_gs[IK_MAX_GATHER_CHUNKS] = {}, ev_ge[IK_MAX_GATHER_CHUNKS] = {};  // gather k
+  hipEvent_t ev_done = nullptr;  // the call's last gather / copy on cs
 };
 
 // The chunked host-pointer pipeline (ik_pipe.cpp): copy streams, per-chunk
@@ -72,9 +89,13 @@ struct ik_ctx {
   IkComm comm;
   IkPipe pipe;
   hipStream_t last_stream = nullptr;  // the stream the last solve was enqueued on
+  hipEvent_t call_done = nullptr;     // recorded on last_stream at the end of every call
+  bool call_done_set = false;
   bool last_sharded = false;  // the last call's stats are in comm.h_tails
   // the gathered tails of the last sharded call (for IK_F_ASYNC + ik_stats_fetch)
   int64_t last_n = 0;
+  bool last_piped = false;  // the last call was a chunked host pipeline: its stats are piped_stats
+  ik_stats piped_stats = {};
 };
 
 namespace ikapi {
@@ -88,10 +109,14 @@ int fail(int code, const std::string &msg);
       return ::ikapi::fail(IK_E_HIP, std::string(#call) + ": " + hipGetErrorString(e_)); \
   } while (0)
 
-// Per-kernel HIP-event timing of the current call (ik_ctx_set_timing).
+// One enqueueing call: per-kernel HIP-event timing of it (ik_ctx_set_timing),
+// and the context's one sequence of device work -- on entry the call's stream
+// waits for the previous call's end event when that call ran on another stream;
+// on exit the call records its own.
 struct KtScope {
   explicit KtScope(ik_ctx *c);
   ~KtScope();
+  ik_ctx *c_;
 };
 
 struct Stage {

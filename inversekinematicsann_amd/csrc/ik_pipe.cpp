@@ -119,7 +119,6 @@ static int merge_chunk_stats(ik_ctx *c, int K, const int64_t *begin, ik_stats *s
   IK_HIP(hipStreamSynchronize(c->pipe.s_out));
   IK_HIP(hipStreamSynchronize(c->stream));
   c->last_sharded = false;
-  if (!stats) return IK_OK;
   ik_shard_tail t[kPipeMaxChunks];
   for (int k = 0; k < K; ++k) {
     ik_stats s;
@@ -134,7 +133,13 @@ static int merge_chunk_stats(ik_ctx *c, int K, const int64_t *begin, ik_stats *s
     t[k].sum_fk_err = s.sum_fk_err;
     t[k].rows = begin[k + 1] - begin[k];
   }
-  return ik_tail_reduce(t, K, stats);
+  // kept on the context: ik_stats_fetch after this call returns them (the
+  // context's own stats block holds no part of a pipelined call)
+  int rc = ik_tail_reduce(t, K, &c->piped_stats);
+  if (rc) return rc;
+  c->last_piped = true;
+  if (stats) *stats = c->piped_stats;
+  return IK_OK;
 }
 
 // One output region: row_bytes per point, host base, device base.

@@ -1,23 +1,34 @@
-// ik_shard.hip -- the batch sharded over GPUs with one RCCL all-gather
-// (include/ikhip.h "multi-GPU").
+// ik_shard.hip -- the batch sharded over GPUs, gathered in place over RCCL in
+// chunks that overlap the solve (include/ikhip.h "multi-GPU").
 //
 // The reference scales by competing consumers (rpc_broker.py:55-68): each worker
 // takes whole requests.  Here the points of one batch are independent, so the
-// batch is split contiguously over the ranks (one process per GPU), every rank
-// solves its rows into one block of a send buffer -- the rows of each output,
-// then a 64-byte tail with its stats -- and ONE ncclAllGather over xGMI hands
-// every rank every block.  The rows go to the caller's arrays in point order
-// (one unpack kernel, or per-rank D2H copies for host arrays) and the stats are
-// reduced on the host from the gathered tails, so no all_reduce is needed: the
-// lowest global failing index, iteration sums and FK-error max/sum all come from
-// the same collective.
+// batch is split over the ranks (one process per GPU) in C chunks of g parts:
+// rank r owns part (c, r) = rows [(c g + r) S, (c g + r + 1) S) of every chunk c,
+// S = ceil(n / (C g)).  Each chunk is contiguous in the caller's arrays and every
+// rank's part of it sits at rank offset r S, which is exactly ncclAllGather's
+// in-place layout (sendbuf = recvbuf + r count): the solve writes its rows at
+// their global position and the all-gather of chunk c fills in the other ranks'
+// rows, on a second stream, while the solve stream runs chunk c + 1.  There is no
+// pack and no unpack kernel; only the ragged last chunk (when C g S > n) is
+// gathered through a staging buffer of g S rows and copied out (its rows are in
+// global order there too, truncated at n).
 //
-// RCCL is loaded at run time (dlopen): the process's own librccl when one is
-// already loaded (torch ships one, built against the HIP runtime the process
-// uses), else librccl.so.1 from the ROCm install.
+// What is gathered per row is what the reference returns: the angles (and the
+// FABRIK iteration counts, the bit-exact integer result).  The per-point FK
+// error stays on its rank; the batch's FK-error max / sum and a 2048-bin
+// histogram (quantiles) travel in a per-rank tail block with the last chunk,
+// beside first_oob / first_err (lowest GLOBAL index: the reference's sequential
+// exception precedence), the iteration sum and the capped count.  No all_reduce.
+//
+// RCCL is loaded at run time (dlopen): a librccl the process already holds
+// (torch ships one, built against the HIP runtime the process uses; found by
+// walking the loaded objects), else librccl.so.1 from the ROCm install.
 #include <dlfcn.h>
+#include <link.h>
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -40,6 +51,7 @@ typedef int (*CommInitRankBlobFn)(void **comm, int nranks, IdBlob id, int rank);
 typedef int (*CommDestroyFn)(void *comm);
 typedef int (*AllGatherFn)(const void *send, void *recv, size_t count, int dtype, void *comm,
                            hipStream_t stream);
+typedef int (*GroupFn)();
 typedef const char *(*GetErrorStringFn)(int);
 constexpr int kNcclUint8 = 1;  // ncclDataType_t ncclUint8
 
@@ -49,12 +61,27 @@ struct Rccl {
   CommInitRankBlobFn comm_init_rank = nullptr;
   CommDestroyFn comm_destroy = nullptr;
   AllGatherFn all_gather = nullptr;
+  GroupFn group_start = nullptr, group_end = nullptr;
   GetErrorStringFn error_string = nullptr;
   std::string where;
 };
 
 std::mutex g_rccl_mu;
 Rccl g_rccl;
+
+// The path of a librccl*.so* already mapped into the process (torch's bundled
+// copy may carry another soname than librccl.so.1), or "".
+int find_loaded_rccl(struct dl_phdr_info *info, size_t, void *data) {
+  const char *p = info->dlpi_name;
+  if (!p || !*p) return 0;
+  const char *base = std::strrchr(p, '/');
+  base = base ? base + 1 : p;
+  if (std::strncmp(base, "librccl", 7) == 0 && std::strstr(base, ".so")) {
+    *static_cast<std::string *>(data) = p;
+    return 1;
+  }
+  return 0;
+}
 
 int load_rccl(Rccl **out) {
   std::lock_guard<std::mutex> lk(g_rccl_mu);
@@ -67,12 +94,11 @@ int load_rccl(Rccl **out) {
       where = over;
     } else {
       // a librccl the process already holds (torch's), then the ROCm one
-      for (const char *nm : {"librccl.so", "librccl.so.1"}) {
-        h = dlopen(nm, RTLD_NOW | RTLD_NOLOAD);
-        if (h) {
-          where = std::string(nm) + " (already loaded)";
-          break;
-        }
+      std::string loaded;
+      dl_iterate_phdr(find_loaded_rccl, &loaded);
+      if (!loaded.empty()) {
+        h = dlopen(loaded.c_str(), RTLD_NOW | RTLD_NOLOAD);
+        where = loaded + " (already loaded)";
       }
       for (const char *nm : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1"}) {
         if (h) break;
@@ -91,10 +117,13 @@ int load_rccl(Rccl **out) {
     r.comm_init_rank = reinterpret_cast<CommInitRankBlobFn>(dlsym(h, "ncclCommInitRank"));
     r.comm_destroy = reinterpret_cast<CommDestroyFn>(dlsym(h, "ncclCommDestroy"));
     r.all_gather = reinterpret_cast<AllGatherFn>(dlsym(h, "ncclAllGather"));
+    r.group_start = reinterpret_cast<GroupFn>(dlsym(h, "ncclGroupStart"));
+    r.group_end = reinterpret_cast<GroupFn>(dlsym(h, "ncclGroupEnd"));
     r.error_string = reinterpret_cast<GetErrorStringFn>(dlsym(h, "ncclGetErrorString"));
-    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_gather)
+    if (!r.get_unique_id || !r.comm_init_rank || !r.comm_destroy || !r.all_gather ||
+        !r.group_start || !r.group_end)
       return fail(IK_E_RCCL, "RCCL at " + where + " lacks ncclGetUniqueId / ncclCommInitRank / "
-                                                  "ncclCommDestroy / ncclAllGather");
+                                                  "ncclCommDestroy / ncclAllGather / ncclGroup*");
     g_rccl = r;
   }
   *out = &g_rccl;
@@ -106,211 +135,276 @@ int rccl_fail(const Rccl *r, const char *what, int res) {
   return fail(IK_E_RCCL, std::string(what) + ": " + msg + " (" + std::to_string(res) + ")");
 }
 
-// floor(r n / g); exact in 64 bits for n g < 2^63 (ik_shard_range checks n < 2^48)
-int64_t shard_begin(int64_t n, int g, int r) { return n * r / g; }
+bool plan_args_ok(int64_t n, int nranks, int chunks) {
+  return n >= 0 && n < ((int64_t)1 << 48) && nranks >= 1 && nranks <= 1024 && chunks >= 1 &&
+         chunks <= IK_MAX_GATHER_CHUNKS;
+}
 
-int64_t up64(int64_t b) { return (b + 63) & ~(int64_t)63; }
+// S = ceil(n / (C g)); the chunks that hold rows; the rows of the full ones.
+void make_plan(int64_t n, int g, int C, ik_shard_plan *p) {
+  std::memset(p, 0, sizeof(*p));
+  p->n = n;
+  p->nranks = g;
+  const int64_t cg = (int64_t)C * g;
+  p->part_rows = n > 0 ? (n + cg - 1) / cg : 0;
+  const int64_t per_chunk = p->part_rows * g;
+  p->chunks = n > 0 ? (int)((n + per_chunk - 1) / per_chunk) : 0;
+  p->full_rows = per_chunk > 0 ? (n / per_chunk) * per_chunk : 0;
+}
+
+void part_of(const ik_shard_plan &p, int r, int c, int64_t *b, int64_t *e) {
+  const int64_t S = p.part_rows;
+  const int64_t lo = ((int64_t)c * p.nranks + r) * S, hi = lo + S;
+  *b = lo < p.n ? lo : p.n;
+  *e = hi < p.n ? hi : p.n;
+}
 
 }  // namespace
 
 namespace ikhip {
 
-// The tail of this rank: the shard's DevStats reduced, indices made global.
-__global__ void pack_tail_kernel(const DevStats *S, int64_t begin, int64_t rows,
-                                 ik_shard_tail *t) {
-  __shared__ unsigned long long s_it[kStatShards], s_cap[kStatShards], s_mx[kStatShards];
-  __shared__ double s_sum[kStatShards];
-  __shared__ int s_mi[kStatShards];
-  const int i = threadIdx.x;
-  if (i < kStatShards) {
-    s_it[i] = S->sum_iters[i];
-    s_cap[i] = S->n_capped[i];
-    s_mx[i] = S->max_fk_err_bits[i];
-    s_sum[i] = S->sum_fk_err[i];
-    s_mi[i] = S->max_iters[i];
+// The rank's FK errors of one part into its tail block's histogram.
+__global__ __launch_bounds__(256) void fk_hist_kernel(const double *err, int64_t n,
+                                                      uint32_t *hist) {
+  __shared__ uint32_t h[IK_FKHIST_BINS];
+  for (int i = threadIdx.x; i < IK_FKHIST_BINS; i += blockDim.x) h[i] = 0;
+  __syncthreads();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int b = fkhist_bin(err[i]);
+    if (b >= 0) atomicAdd(&h[b], 1u);
   }
   __syncthreads();
-  if (i != 0) return;
+  for (int i = threadIdx.x; i < IK_FKHIST_BINS; i += blockDim.x)
+    if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+// The rank's tail: its chunks' DevStats merged, indices made global (the
+// chunks are in increasing global order, so the first chunk holding a failure
+// holds the rank's lowest failing index).
+struct TailArgs {
+  const DevStats *S;  // K blocks
+  int K;
+  int64_t base[IK_MAX_GATHER_CHUNKS];  // global row of each chunk's part's first row
+  int64_t rows;
+};
+
+__global__ void pack_tail_kernel(TailArgs a, ik_shard_tail *t) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
   ik_shard_tail o;
-  o.first_oob = S->first_oob == ~0ull ? -1 : (int64_t)S->first_oob + begin;
-  if (S->first_err_key == ~0ull) {
-    o.first_err = -1;
-    o.first_err_code = IK_OK;
-  } else {
-    o.first_err = (int64_t)(S->first_err_key >> 8) + begin;
-    o.first_err_code = (int32_t)(S->first_err_key & 0xff);
-  }
+  o.first_oob = -1;
+  o.first_err = -1;
+  o.first_err_code = IK_OK;
   o.max_iters = 0;
   o.sum_iters = 0;
   o.n_capped = 0;
   o.max_fk_err = 0.0;
   o.sum_fk_err = 0.0;
-  for (int k = 0; k < kStatShards; ++k) {  // the shard order of stats_from_dev
-    o.max_iters = s_mi[k] > o.max_iters ? s_mi[k] : o.max_iters;
-    o.sum_iters += (int64_t)s_it[k];
-    o.n_capped += (int64_t)s_cap[k];
-    const double mx = __longlong_as_double((long long)s_mx[k]);
-    o.max_fk_err = mx > o.max_fk_err ? mx : o.max_fk_err;
-    o.sum_fk_err += s_sum[k];
-  }
-  o.rows = rows;
-  *t = o;
-}
-
-// Gathered blocks -> the caller's arrays in point order: row i belongs to rank
-// r = ceil((i + 1) g / n) - 1 (the r with floor(r n / g) <= i < floor((r + 1) n / g)).
-struct Unpack {
-  const char *recv;
-  int64_t block, n;
-  int g, nreg;
-  int64_t off[3];
-  int words[3];  // 4-byte words per row of each region
-  char *dst[3];
-};
-
-__global__ __launch_bounds__(256) void gather_unpack_kernel(Unpack u) {
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < u.n; i += stride) {
-    const int r = (int)(((i + 1) * u.g + u.n - 1) / u.n) - 1;
-    const int64_t local = i - u.n * r / u.g;
-    const char *blk = u.recv + (int64_t)r * u.block;
-    for (int q = 0; q < u.nreg; ++q) {
-      const uint32_t *s =
-          reinterpret_cast<const uint32_t *>(blk + u.off[q]) + local * u.words[q];
-      uint32_t *d = reinterpret_cast<uint32_t *>(u.dst[q]) + i * u.words[q];
-      if (u.words[q] == 4) {
-        *reinterpret_cast<uint4 *>(d) = *reinterpret_cast<const uint4 *>(s);
-      } else if (u.words[q] == 8) {
-        reinterpret_cast<uint4 *>(d)[0] = reinterpret_cast<const uint4 *>(s)[0];
-        reinterpret_cast<uint4 *>(d)[1] = reinterpret_cast<const uint4 *>(s)[1];
-      } else {
-        for (int w = 0; w < u.words[q]; ++w) d[w] = s[w];
-      }
+  for (int k = 0; k < a.K; ++k) {
+    const DevStats *S = a.S + k;
+    if (o.first_oob < 0 && S->first_oob != ~0ull) o.first_oob = (int64_t)S->first_oob + a.base[k];
+    if (o.first_err < 0 && S->first_err_key != ~0ull) {
+      o.first_err = (int64_t)(S->first_err_key >> 8) + a.base[k];
+      o.first_err_code = (int32_t)(S->first_err_key & 0xff);
+    }
+    for (int s = 0; s < kStatShards; ++s) {  // the shard order of stats_from_dev
+      o.max_iters = S->max_iters[s] > o.max_iters ? S->max_iters[s] : o.max_iters;
+      o.sum_iters += (int64_t)S->sum_iters[s];
+      o.n_capped += (int64_t)S->n_capped[s];
+      const double mx = __longlong_as_double((long long)S->max_fk_err_bits[s]);
+      o.max_fk_err = mx > o.max_fk_err ? mx : o.max_fk_err;
+      o.sum_fk_err += S->sum_fk_err[s];
     }
   }
+  o.rows = a.rows;
+  *t = o;
 }
 
 }  // namespace ikhip
 
 namespace {
 
-// Bytes of the regions: angles first (16-byte aligned rows for the kernels'
-// 16-byte stores), then iterations / FK errors, each region 64-byte aligned.
-void layout(int method, int64_t n, int g, bool with_iters, bool with_fk, ik_gather_layout *L) {
-  std::memset(L, 0, sizeof(*L));
-  const int64_t S = g > 0 ? (n + g - 1) / g : 0;  // >= the largest floor-split shard
-  L->shard = S;
-  int k = 0;
-  int64_t off = 0;
-  auto add = [&](int rb) {
-    L->row_bytes[k] = rb;
-    L->offset[k] = off;
-    off = up64(off + S * rb);
-    ++k;
-  };
-  add(method == IK_METHOD_ANN ? 16 : 32);
-  if (with_iters) add(4);
-  if (with_fk) add(8);
-  L->nregion = k;
-  L->tail_offset = off;
-  L->block_bytes = up64(off + (int64_t)sizeof(ik_shard_tail));
+int auto_chunks(ik_ctx *c, int method, int64_t n) {
+  const IkComm &m = c->comm;
+  int C = m.chunks_req;
+  if (C <= 0) {
+    static int env = -1;
+    if (env < 0) {
+      const char *e = std::getenv("IKHIP_GATHER_CHUNKS");
+      env = (e && *e) ? std::atoi(e) : 0;
+    }
+    C = env;
+  }
+  if (C <= 0)  // automatic: overlap only where the gather is comparable to the solve
+    C = (method == IK_METHOD_FABRIK && m.nranks > 1 && n / m.nranks >= 262144) ? 4 : 1;
+  return C > IK_MAX_GATHER_CHUNKS ? IK_MAX_GATHER_CHUNKS : C;
 }
 
-int ensure_comm_buffers(ik_ctx *c, size_t send, size_t recv) {
+int ensure_comm_state(ik_ctx *c, size_t stage) {
   IkComm &m = c->comm;
-  if (send > m.send_bytes || recv > m.recv_bytes || m.h_tails_n < m.nranks) {
-    IK_HIP(hipStreamSynchronize(c->stream));
+  if (!m.cs) {
+    IK_HIP(hipStreamCreateWithFlags(&m.cs, hipStreamNonBlocking));
+    for (int k = 0; k < IK_MAX_GATHER_CHUNKS; ++k) {
+      IK_HIP(hipEventCreateWithFlags(&m.ev_solved[k], hipEventDisableTiming));
+      IK_HIP(hipEventCreate(&m.ev_gs[k]));
+      IK_HIP(hipEventCreate(&m.ev_ge[k]));
+    }
+    IK_HIP(hipEventCreateWithFlags(&m.ev_done, hipEventDisableTiming));
+    IK_HIP(hipMalloc(&m.d_cstats, sizeof(DevStats) * IK_MAX_GATHER_CHUNKS));
+    IK_HIP(hipMalloc(&m.tail_send, sizeof(IkTailBlock)));
   }
-  if (send > m.send_bytes) {
-    if (m.send) IK_HIP(hipFree(m.send));
-    m.send = nullptr;
-    m.send_bytes = 0;
-    IK_HIP(hipMalloc(&m.send, send));
-    m.send_bytes = send;
+  // the previous call's gathers finished before its solve stream did (it waited
+  // for ev_done), so syncing that stream frees every buffer below
+  if (stage > m.stage_bytes || m.tails_n < m.nranks) IK_HIP(hipStreamSynchronize(c->stream));
+  if (stage > m.stage_bytes) {
+    if (m.stage) IK_HIP(hipFree(m.stage));
+    m.stage = nullptr;
+    m.stage_bytes = 0;
+    IK_HIP(hipMalloc(&m.stage, stage));
+    m.stage_bytes = stage;
   }
-  if (recv > m.recv_bytes) {
-    if (m.recv) IK_HIP(hipFree(m.recv));
-    m.recv = nullptr;
-    m.recv_bytes = 0;
-    IK_HIP(hipMalloc(&m.recv, recv));
-    m.recv_bytes = recv;
-  }
-  if (m.h_tails_n < m.nranks) {
+  if (m.tails_n < m.nranks) {
+    if (m.tail_recv) IK_HIP(hipFree(m.tail_recv));
     if (m.h_tails) IK_HIP(hipHostFree(m.h_tails));
+    m.tail_recv = nullptr;
     m.h_tails = nullptr;
+    m.tails_n = 0;
+    IK_HIP(hipMalloc(&m.tail_recv, sizeof(IkTailBlock) * (size_t)m.nranks));
     IK_HIP(hipHostMalloc(reinterpret_cast<void **>(&m.h_tails),
-                         sizeof(ik_shard_tail) * (size_t)m.nranks, hipHostMallocDefault));
-    m.h_tails_n = m.nranks;
+                         sizeof(IkTailBlock) * (size_t)m.nranks, hipHostMallocDefault));
+    m.tails_n = m.nranks;
   }
-  if (!m.g0) IK_HIP(hipEventCreate(&m.g0));
-  if (!m.g1) IK_HIP(hipEventCreate(&m.g1));
   return IK_OK;
 }
 
-// After the solve wrote this rank's rows into its send block: the tail, the
-// all-gather, the rows to the caller's arrays, the tails to the host.
-int gather_and_unpack(ik_ctx *c, const ik_gather_layout &L, int64_t n, int64_t begin,
-                      int64_t rows, char *const dst[3], bool dev) {
+// One gathered output: row bytes, the caller-visible device rows (n of them;
+// the caller's array, or device scratch for host pointers), the staging rows of
+// the ragged chunk.
+struct Region {
+  int rb;
+  char *out;
+  char *stage;
+};
+
+// The solve of one part: rows [b, b + m) of the batch; `at(q)` is where
+// region q's first row goes; fk_err (device, nullable) the part's FK errors;
+// S the chunk's stats block.
+struct PartJob {
+  int64_t b, m;
+  char *at[2];
+  double *fk_err;
+  DevStats *S;
+};
+
+// The whole sharded call after argument checks: per chunk, the solve of this
+// rank's part on the context's stream, then the in-place all-gather of the
+// chunk on the comm stream; the tail block with the last chunk; the ragged
+// chunk's rows out of the stage; the solve stream waits for the gathers.
+template <class Solve>
+int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nreg,
+                double *fk_err_dev, Solve solve) {
   IkComm &m = c->comm;
   Rccl *r = nullptr;
   int rc = load_rccl(&r);
   if (rc) return rc;
-  char *send = static_cast<char *>(m.send);
-  char *recv = static_cast<char *>(m.recv);
-  hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, c->d_stats, begin, rows,
-                     reinterpret_cast<ik_shard_tail *>(send + L.tail_offset));
-  IK_HIP(hipGetLastError());
-  kt_begin("rccl_all_gather", c->stream);
-  IK_HIP(hipEventRecord(m.g0, c->stream));
-  const int res = r->all_gather(send, recv, (size_t)L.block_bytes, kNcclUint8, m.comm, c->stream);
-  if (res != 0) return rccl_fail(r, "ncclAllGather", res);
-  IK_HIP(hipEventRecord(m.g1, c->stream));
-  kt_end(c->stream);
-  if (dev) {
-    Unpack u;
-    std::memset(&u, 0, sizeof(u));
-    u.recv = recv;
-    u.block = L.block_bytes;
-    u.n = n;
-    u.g = m.nranks;
-    u.nreg = 0;
-    for (int q = 0; q < L.nregion; ++q) {
-      if (!dst[q]) continue;
-      u.off[u.nreg] = L.offset[q];
-      u.words[u.nreg] = L.row_bytes[q] / 4;
-      u.dst[u.nreg] = dst[q];
-      ++u.nreg;
+  const int g = m.nranks, me = m.rank, C = P.chunks;
+  const int64_t S = P.part_rows;
+  m.last_chunks = C;
+  m.last_hist = fk_err_dev != nullptr;
+  // the tail block: zeroed (histogram) before any part adds to it
+  IK_HIP(hipMemsetAsync(m.tail_send, 0, sizeof(IkTailBlock), c->stream));
+  TailArgs ta;
+  std::memset(&ta, 0, sizeof(ta));
+  ta.S = m.d_cstats;
+  ta.K = C;
+  for (int k = 0; k < C; ++k) {
+    int64_t b, e;
+    part_of(P, me, k, &b, &e);
+    const int64_t cb = (int64_t)k * g * S;  // the chunk's first row
+    const bool staged = cb + g * S > P.n;  // the ragged last chunk
+    PartJob j;
+    j.b = b;
+    j.m = e - b;
+    for (int q = 0; q < 2; ++q)
+      j.at[q] = q < nreg ? (staged ? R[q].stage + (int64_t)me * S * R[q].rb
+                                   : R[q].out + b * R[q].rb)
+                         : nullptr;
+    j.fk_err = fk_err_dev ? fk_err_dev + b : nullptr;
+    j.S = m.d_cstats + k;
+    ta.base[k] = b;
+    ta.rows += j.m;
+    if (j.m > 0) {
+      if ((rc = solve(j))) return rc;
+      if (j.fk_err) {
+        const int64_t want = (j.m + 2047) / 2048;
+        kt_begin("fk_hist_kernel", c->stream);
+        hipLaunchKernelGGL(fk_hist_kernel, dim3((unsigned)(want < 512 ? want : 512)), dim3(256),
+                           0, c->stream, j.fk_err, j.m, m.tail_send->hist);
+        kt_end(c->stream);
+      }
+    } else {
+      launch_reset_stats(j.S, c->stream);  // an empty part: zero stats for the tail
     }
-    if (u.nreg && n > 0) {
-      int cus = 256, dv = 0;
-      (void)hipGetDevice(&dv);
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dv);
-      const int64_t want = (n + 255) / 256, cap = (int64_t)(cus > 0 ? cus : 256) * 8;
-      kt_begin("gather_unpack_kernel", c->stream);
-      hipLaunchKernelGGL(gather_unpack_kernel, dim3((unsigned)(want < cap ? want : cap)),
-                         dim3(256), 0, c->stream, u);
-      kt_end(c->stream);
-      IK_HIP(hipGetLastError());
+    const bool last = k == C - 1;
+    if (last) {
+      hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, &m.tail_send->t);
     }
-  } else {
-    for (int rr = 0; rr < m.nranks; ++rr) {
-      const int64_t b = shard_begin(n, m.nranks, rr), e = shard_begin(n, m.nranks, rr + 1);
-      if (e <= b) continue;
-      for (int q = 0; q < L.nregion; ++q) {
-        if (!dst[q]) continue;
-        IK_HIP(hipMemcpyAsync(dst[q] + b * L.row_bytes[q],
-                              recv + (int64_t)rr * L.block_bytes + L.offset[q],
-                              (size_t)(e - b) * L.row_bytes[q], hipMemcpyDeviceToHost,
-                              c->stream));
+    IK_HIP(hipGetLastError());
+    IK_HIP(hipEventRecord(m.ev_solved[k], c->stream));
+    IK_HIP(hipStreamWaitEvent(m.cs, m.ev_solved[k], 0));
+    // chunk k's rows of every rank, in place (+ every rank's tail block with the last)
+    kt_begin("rccl_all_gather", m.cs);
+    IK_HIP(hipEventRecord(m.ev_gs[k], m.cs));
+    int res = r->group_start();
+    if (res != 0) return rccl_fail(r, "ncclGroupStart", res);
+    for (int q = 0; q < nreg; ++q) {
+      char *base = staged ? R[q].stage : R[q].out + cb * R[q].rb;
+      const size_t cnt = (size_t)S * R[q].rb;
+      res = r->all_gather(base + (size_t)me * cnt, base, cnt, kNcclUint8, m.comm, m.cs);
+      if (res != 0) {
+        (void)r->group_end();
+        return rccl_fail(r, "ncclAllGather", res);
       }
     }
+    if (last) {
+      res = r->all_gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), kNcclUint8, m.comm, m.cs);
+      if (res != 0) {
+        (void)r->group_end();
+        return rccl_fail(r, "ncclAllGather", res);
+      }
+    }
+    res = r->group_end();
+    if (res != 0) return rccl_fail(r, "ncclGroupEnd", res);
+    IK_HIP(hipEventRecord(m.ev_ge[k], m.cs));
+    kt_end(m.cs);
+    if (staged && cb < P.n)  // the ragged chunk: its rows are in global order in the stage
+      for (int q = 0; q < nreg; ++q)
+        IK_HIP(hipMemcpyAsync(R[q].out + cb * R[q].rb, R[q].stage, (size_t)(P.n - cb) * R[q].rb,
+                              hipMemcpyDeviceToDevice, m.cs));
   }
-  // every rank's tail to the host (the stats; read by sharded_stats)
-  IK_HIP(hipMemcpy2DAsync(m.h_tails, sizeof(ik_shard_tail), recv + L.tail_offset,
-                          (size_t)L.block_bytes, sizeof(ik_shard_tail), (size_t)m.nranks,
-                          hipMemcpyDeviceToHost, c->stream));
+  if (C == 0) {  // an empty batch: every rank still exchanges its (empty) tail
+    launch_reset_stats(m.d_cstats, c->stream);
+    ta.K = 1;
+    hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, &m.tail_send->t);
+    IK_HIP(hipGetLastError());
+    IK_HIP(hipEventRecord(m.ev_solved[0], c->stream));
+    IK_HIP(hipStreamWaitEvent(m.cs, m.ev_solved[0], 0));
+    IK_HIP(hipEventRecord(m.ev_gs[0], m.cs));
+    const int res =
+        r->all_gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), kNcclUint8, m.comm, m.cs);
+    if (res != 0) return rccl_fail(r, "ncclAllGather", res);
+    IK_HIP(hipEventRecord(m.ev_ge[0], m.cs));
+    m.last_chunks = 1;
+  }
+  // the call ends on the solve stream: it waits for the gathers, then the tails
+  // go to the host
+  IK_HIP(hipEventRecord(m.ev_done, m.cs));
+  IK_HIP(hipStreamWaitEvent(c->stream, m.ev_done, 0));
+  IK_HIP(hipMemcpyAsync(m.h_tails, m.tail_recv, sizeof(IkTailBlock) * (size_t)g,
+                        hipMemcpyDeviceToHost, c->stream));
   c->last_sharded = true;
-  c->last_n = n;
+  c->last_n = P.n;
+  (void)method;
   return IK_OK;
 }
 
@@ -321,25 +415,42 @@ namespace ikapi {
 int sharded_stats(ik_ctx *c, ik_stats *stats) {
   IK_HIP(hipStreamSynchronize(c->stream));
   if (!stats) return IK_OK;
-  int rc = ik_tail_reduce(c->comm.h_tails, c->comm.nranks, stats);
+  IkComm &m = c->comm;
+  ik_shard_tail t[1024];
+  for (int r = 0; r < m.nranks; ++r) t[r] = m.h_tails[r].t;
+  int rc = ik_tail_reduce(t, m.nranks, stats);
   if (rc) return rc;
-  float ms = 0.0f;
-  if (hipEventElapsedTime(&ms, c->comm.g0, c->comm.g1) == hipSuccess) stats->gather_ms = ms;
+  float tot = 0.0f;
+  for (int k = 0; k < m.last_chunks; ++k) {
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, m.ev_gs[k], m.ev_ge[k]) == hipSuccess) tot += ms;
+  }
+  stats->gather_ms = tot;
   return IK_OK;
 }
 
 void comm_release(ik_ctx *c) {
   IkComm &m = c->comm;
+  if (m.cs) (void)hipStreamSynchronize(m.cs);
   if (m.comm) {
     Rccl *r = nullptr;
     if (load_rccl(&r) == IK_OK) (void)r->comm_destroy(m.comm);
   }
-  if (m.send) (void)hipFree(m.send);
-  if (m.recv) (void)hipFree(m.recv);
+  if (m.stage) (void)hipFree(m.stage);
+  if (m.tail_send) (void)hipFree(m.tail_send);
+  if (m.tail_recv) (void)hipFree(m.tail_recv);
   if (m.h_tails) (void)hipHostFree(m.h_tails);
-  if (m.g0) (void)hipEventDestroy(m.g0);
-  if (m.g1) (void)hipEventDestroy(m.g1);
+  if (m.d_cstats) (void)hipFree(m.d_cstats);
+  for (int k = 0; k < IK_MAX_GATHER_CHUNKS; ++k) {
+    if (m.ev_solved[k]) (void)hipEventDestroy(m.ev_solved[k]);
+    if (m.ev_gs[k]) (void)hipEventDestroy(m.ev_gs[k]);
+    if (m.ev_ge[k]) (void)hipEventDestroy(m.ev_ge[k]);
+  }
+  if (m.ev_done) (void)hipEventDestroy(m.ev_done);
+  if (m.cs) (void)hipStreamDestroy(m.cs);
+  const int keep_chunks = m.chunks_req;
   m = IkComm();
+  m.chunks_req = keep_chunks;
   c->last_sharded = false;
 }
 
@@ -360,12 +471,13 @@ int ik_comm_unique_id(uint8_t *id) {
 }
 
 int ik_comm_init(ik_ctx *c, int nranks, int rank, const uint8_t *id) {
-  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks)
+  if (!c || !id || nranks < 1 || nranks > 1024 || rank < 0 || rank >= nranks)
     return fail(IK_E_BADARG, "ik_comm_init: bad args");
   int rc = set_dev(c);
   if (rc) return rc;
   Rccl *r = nullptr;
   if ((rc = load_rccl(&r))) return rc;
+  (void)hipStreamSynchronize(c->stream);
   comm_release(c);
   IdBlob b;
   std::memcpy(b.b, id, IK_COMM_ID_BYTES);
@@ -387,21 +499,42 @@ int ik_comm_destroy(ik_ctx *c) {
   return IK_OK;
 }
 
-int ik_shard_range(int64_t n, int nranks, int rank, int64_t *begin, int64_t *end) {
-  if (n < 0 || n >= ((int64_t)1 << 48) || nranks < 1 || nranks > 1024 || rank < 0 ||
-      rank >= nranks || !begin || !end)
-    return fail(IK_E_BADARG, "ik_shard_range: bad args");
-  *begin = shard_begin(n, nranks, rank);
-  *end = shard_begin(n, nranks, rank + 1);
+int ik_comm_info(ik_ctx *c, int *nranks, int *rank, int *last_chunks) {
+  if (!c) return fail(IK_E_BADARG, "ik_comm_info: NULL context");
+  if (nranks) *nranks = c->comm.comm ? c->comm.nranks : 0;
+  if (rank) *rank = c->comm.comm ? c->comm.rank : -1;
+  if (last_chunks) *last_chunks = c->comm.last_req;
   return IK_OK;
 }
 
-int ik_gather_layout_of(int method, int64_t n, int nranks, int with_iters, int with_fk_err,
-                        ik_gather_layout *out) {
-  if (!out || n < 0 || n >= ((int64_t)1 << 48) || nranks < 1 || nranks > 1024 || (method != IK_METHOD_ANN && method != IK_METHOD_FABRIK) ||
-      (method == IK_METHOD_ANN && with_iters))
-    return fail(IK_E_BADARG, "ik_gather_layout_of: bad args");
-  layout(method, n, nranks, with_iters != 0, with_fk_err != 0, out);
+int ik_comm_set_chunks(ik_ctx *c, int chunks) {
+  if (!c || chunks < 0 || chunks > IK_MAX_GATHER_CHUNKS)
+    return fail(IK_E_BADARG, "ik_comm_set_chunks: chunks must be 0.." +
+                                 std::to_string(IK_MAX_GATHER_CHUNKS));
+  c->comm.chunks_req = chunks;
+  return IK_OK;
+}
+
+int ik_shard_plan_of(int64_t n, int nranks, int chunks, ik_shard_plan *out) {
+  if (!out || !plan_args_ok(n, nranks, chunks)) return fail(IK_E_BADARG, "ik_shard_plan_of: bad args");
+  make_plan(n, nranks, chunks, out);
+  return IK_OK;
+}
+
+int ik_shard_part(const ik_shard_plan *p, int rank, int chunk, int64_t *begin, int64_t *end) {
+  if (!p || !begin || !end || rank < 0 || rank >= p->nranks || chunk < 0 ||
+      chunk >= IK_MAX_GATHER_CHUNKS)
+    return fail(IK_E_BADARG, "ik_shard_part: bad args");
+  part_of(*p, rank, chunk, begin, end);
+  return IK_OK;
+}
+
+int ik_shard_range(int64_t n, int nranks, int rank, int64_t *begin, int64_t *end) {
+  if (!plan_args_ok(n, nranks, 1) || rank < 0 || rank >= nranks || !begin || !end)
+    return fail(IK_E_BADARG, "ik_shard_range: bad args");
+  ik_shard_plan p;
+  make_plan(n, nranks, 1, &p);
+  part_of(p, rank, 0, begin, end);
   return IK_OK;
 }
 
@@ -429,13 +562,102 @@ int ik_tail_reduce(const ik_shard_tail *t, int nranks, ik_stats *s) {
   return IK_OK;
 }
 
+int ik_fkhist_bin(double e) { return fkhist_bin(e); }
+
+double ik_fkhist_upper(int bin) {
+  if (bin < 0 || bin >= IK_FKHIST_BINS - 1) return bin < 0 ? 0.0 : HUGE_VAL;
+  return std::ldexp(1.0 + (double)(bin % 16 + 1) / 16.0, bin / 16 - 64);
+}
+
+int ik_fk_err_quantile(ik_ctx *c, double q, double *out) {
+  if (!c || !out || !(q > 0.0 && q <= 1.0)) return fail(IK_E_BADARG, "ik_fk_err_quantile: bad args");
+  if (!c->last_sharded || !c->comm.last_hist)
+    return fail(IK_E_BADARG, "ik_fk_err_quantile: the last call was not a sharded solve with fk_err");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  IK_HIP(hipStreamSynchronize(c->last_stream ? c->last_stream : c->stream));
+  const IkComm &m = c->comm;
+  uint64_t tot = 0;
+  for (int r = 0; r < m.nranks; ++r)
+    for (int b = 0; b < IK_FKHIST_BINS; ++b) tot += m.h_tails[r].hist[b];
+  *out = NAN;
+  if (tot == 0) return IK_OK;
+  const uint64_t want = (uint64_t)std::ceil(q * (double)tot);
+  uint64_t cum = 0;
+  for (int b = 0; b < IK_FKHIST_BINS; ++b) {
+    for (int r = 0; r < m.nranks; ++r) cum += m.h_tails[r].hist[b];
+    if (cum >= (want ? want : 1)) {
+      *out = ik_fkhist_upper(b);
+      break;
+    }
+  }
+  return IK_OK;
+}
+
 static int sharded_common(ik_ctx *c, int flags, const char *who) {
   if (!c) return fail(IK_E_BADARG, std::string(who) + ": NULL context");
   if (!c->comm.comm) return fail(IK_E_BADARG, std::string(who) + ": no communicator (ik_comm_init)");
-  if (c->comm.nranks > 1024) return fail(IK_E_BADARG, std::string(who) + ": more than 1024 ranks");
   if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
     return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
   return set_dev(c);
+}
+
+// Host pointers: device scratch holds the points (the rank's parts, at their
+// global rows), the gathered outputs (n rows each) and the FK errors.
+struct HostStage {
+  char *pts, *out[2], *fk;
+};
+
+static int host_stage(ik_ctx *c, const ik_shard_plan &P, int64_t n, const int *rb, int nreg,
+                      bool fk, size_t extra, HostStage *h, char **extra_at) {
+  const size_t b_pts = Stage::up((size_t)n * 24);
+  size_t b_out[2] = {0, 0};
+  for (int q = 0; q < nreg; ++q) b_out[q] = Stage::up((size_t)n * rb[q]);
+  const size_t b_fk = fk ? Stage::up((size_t)n * 8) : 0;
+  int rc = ensure_scratch(c, extra + b_pts + b_out[0] + b_out[1] + b_fk);
+  if (rc) return rc;
+  char *s = static_cast<char *>(c->scratch);
+  *extra_at = s;
+  s += extra;
+  h->pts = s;
+  s += b_pts;
+  for (int q = 0; q < 2; ++q) {
+    h->out[q] = q < nreg ? s : nullptr;
+    s += b_out[q];
+  }
+  h->fk = fk ? s : nullptr;
+  (void)P;
+  return IK_OK;
+}
+
+// The rank's parts of the points, host -> scratch at their global rows.
+static int host_points_in(ik_ctx *c, const ik_shard_plan &P, const double *pts, char *dst) {
+  for (int k = 0; k < P.chunks; ++k) {
+    int64_t b, e;
+    part_of(P, c->comm.rank, k, &b, &e);
+    if (e > b)
+      IK_HIP(hipMemcpyAsync(dst + b * 24, pts + 3 * b, (size_t)(e - b) * 24,
+                            hipMemcpyHostToDevice, c->stream));
+  }
+  return IK_OK;
+}
+
+// After the call: the gathered rows (all n) and this rank's FK errors to the host.
+static int host_results_out(ik_ctx *c, const ik_shard_plan &P, const Region *R, int nreg,
+                            char *const *host_out, const char *dfk, double *hfk) {
+  for (int q = 0; q < nreg; ++q)
+    if (host_out[q] && P.n > 0)
+      IK_HIP(hipMemcpyAsync(host_out[q], R[q].out, (size_t)P.n * R[q].rb, hipMemcpyDeviceToHost,
+                            c->stream));
+  if (hfk)
+    for (int k = 0; k < P.chunks; ++k) {
+      int64_t b, e;
+      part_of(P, c->comm.rank, k, &b, &e);
+      if (e > b)
+        IK_HIP(hipMemcpyAsync(hfk + b, dfk + b * 8, (size_t)(e - b) * 8, hipMemcpyDeviceToHost,
+                              c->stream));
+    }
+  return IK_OK;
 }
 
 int ik_ann_solve_sharded(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk_err,
@@ -449,25 +671,35 @@ int ik_ann_solve_sharded(ik_ctx *c, const double *pts, int64_t n, float *ang, do
   if (!c->ann_loaded) return fail(IK_E_NOMODEL, "ik_ann_solve_sharded: no model loaded");
   KtScope kts(c);
   const bool dev = flags & IK_F_DEVICE;
-  const int g = c->comm.nranks, me = c->comm.rank;
-  ik_gather_layout L;
-  layout(IK_METHOD_ANN, n, g, false, fk_err != nullptr, &L);
-  const int64_t b = shard_begin(n, g, me), rows = shard_begin(n, g, me + 1) - b;
-  if ((rc = ensure_comm_buffers(c, (size_t)L.block_bytes, (size_t)L.block_bytes * g))) return rc;
-  char *send = static_cast<char *>(c->comm.send);
-  const double *dp = pts + 3 * b;
+  const int g = c->comm.nranks;
+  ik_shard_plan P;
+  c->comm.last_req = auto_chunks(c, IK_METHOD_ANN, n);
+  make_plan(n, g, c->comm.last_req, &P);
+  const size_t stage = Stage::up((size_t)P.part_rows * g * 16);
+  if ((rc = ensure_comm_state(c, stage))) return rc;
+  Region R[1] = {{16, reinterpret_cast<char *>(ang), static_cast<char *>(c->comm.stage)}};
+  const double *dp = pts;
+  double *dfk = fk_err;
+  HostStage hs;
   if (!dev) {
-    if ((rc = ensure_scratch(c, Stage::up((size_t)rows * 24) + 256))) return rc;
-    if (rows > 0)
-      IK_HIP(hipMemcpyAsync(c->scratch, dp, (size_t)rows * 24, hipMemcpyHostToDevice, c->stream));
-    dp = static_cast<const double *>(c->scratch);
+    const int rb[1] = {16};
+    char *unused = nullptr;
+    if ((rc = host_stage(c, P, n, rb, 1, fk_err != nullptr, 0, &hs, &unused))) return rc;
+    if ((rc = host_points_in(c, P, pts, hs.pts))) return rc;
+    dp = reinterpret_cast<const double *>(hs.pts);
+    R[0].out = hs.out[0];
+    dfk = reinterpret_cast<double *>(hs.fk);
   }
-  // this rank's rows straight into its send block
-  float *da = reinterpret_cast<float *>(send + L.offset[0]);
-  double *de = fk_err ? reinterpret_cast<double *>(send + L.offset[1]) : nullptr;
-  if ((rc = ann_launch(c, dp, rows, da, de, !(flags & IK_F_NO_LIMITS)))) return rc;
-  char *dst[3] = {reinterpret_cast<char *>(ang), reinterpret_cast<char *>(fk_err), nullptr};
-  if ((rc = gather_and_unpack(c, L, n, b, rows, dst, dev))) return rc;
+  const bool limits = !(flags & IK_F_NO_LIMITS);
+  rc = sharded_run(c, IK_METHOD_ANN, P, R, 1, dfk, [&](const PartJob &j) {
+    return ann_launch(c, dp + 3 * j.b, j.m, reinterpret_cast<float *>(j.at[0]), j.fk_err, limits,
+                      j.S);
+  });
+  if (rc) return rc;
+  if (!dev) {
+    char *ho[1] = {reinterpret_cast<char *>(ang)};
+    if ((rc = host_results_out(c, P, R, 1, ho, hs.fk, fk_err))) return rc;
+  }
   if (flags & IK_F_ASYNC) return IK_OK;
   return sharded_stats(c, stats);
 }
@@ -483,34 +715,45 @@ int ik_fabrik_solve_sharded(ik_ctx *c, const double *pts, int64_t n, double tol,
     return fail(IK_E_BADARG, "ik_fabrik_solve_sharded: device ang must be 16-byte aligned");
   KtScope kts(c);
   const bool dev = flags & IK_F_DEVICE;
-  const int g = c->comm.nranks, me = c->comm.rank;
-  ik_gather_layout L;
-  layout(IK_METHOD_FABRIK, n, g, iters != nullptr, fk_err != nullptr, &L);
-  const int64_t b = shard_begin(n, g, me), rows = shard_begin(n, g, me + 1) - b;
-  if ((rc = ensure_comm_buffers(c, (size_t)L.block_bytes, (size_t)L.block_bytes * g))) return rc;
-  char *send = static_cast<char *>(c->comm.send);
-  const size_t b_work = Stage::up(fabrik_scratch_bytes(rows));
-  const size_t b_in = dev ? 0 : Stage::up((size_t)rows * 24);
-  if ((rc = ensure_scratch(c, b_work + b_in))) return rc;
-  char *s = static_cast<char *>(c->scratch);
-  const double *dp = pts + 3 * b;
+  const int g = c->comm.nranks;
+  ik_shard_plan P;
+  c->comm.last_req = auto_chunks(c, IK_METHOD_FABRIK, n);
+  make_plan(n, g, c->comm.last_req, &P);
+  const int nreg = iters ? 2 : 1;
+  const size_t b_ang_st = Stage::up((size_t)P.part_rows * g * 32);
+  const size_t stage = b_ang_st + (iters ? Stage::up((size_t)P.part_rows * g * 4) : 0);
+  if ((rc = ensure_comm_state(c, stage))) return rc;
+  char *st = static_cast<char *>(c->comm.stage);
+  Region R[2] = {{32, reinterpret_cast<char *>(ang), st},
+                 {4, reinterpret_cast<char *>(iters), st + b_ang_st}};
+  const size_t b_work = Stage::up(fabrik_scratch_bytes(P.part_rows));
+  const double *dp = pts;
+  double *dfk = fk_err;
+  char *work = nullptr;
+  HostStage hs;
   if (!dev) {
-    if (rows > 0)
-      IK_HIP(hipMemcpyAsync(s + b_work, dp, (size_t)rows * 24, hipMemcpyHostToDevice, c->stream));
-    dp = reinterpret_cast<const double *>(s + b_work);
+    const int rb[2] = {32, 4};
+    if ((rc = host_stage(c, P, n, rb, nreg, fk_err != nullptr, b_work, &hs, &work))) return rc;
+    if ((rc = host_points_in(c, P, pts, hs.pts))) return rc;
+    dp = reinterpret_cast<const double *>(hs.pts);
+    R[0].out = hs.out[0];
+    if (iters) R[1].out = hs.out[1];
+    dfk = reinterpret_cast<double *>(hs.fk);
+  } else {
+    if ((rc = ensure_scratch(c, b_work))) return rc;
+    work = static_cast<char *>(c->scratch);
   }
-  int q = 0;
-  double *da = reinterpret_cast<double *>(send + L.offset[q++]);
-  int32_t *di = iters ? reinterpret_cast<int32_t *>(send + L.offset[q++]) : nullptr;
-  double *dfe = fk_err ? reinterpret_cast<double *>(send + L.offset[q++]) : nullptr;
-  if ((rc = fabrik_launch(c, dp, rows, tol, max_iter, da, di, nullptr, dfe,
-                          !(flags & IK_F_NO_LIMITS), s)))
-    return rc;
-  char *dst[3] = {reinterpret_cast<char *>(ang), nullptr, nullptr};
-  q = 1;
-  if (iters) dst[q++] = reinterpret_cast<char *>(iters);
-  if (fk_err) dst[q++] = reinterpret_cast<char *>(fk_err);
-  if ((rc = gather_and_unpack(c, L, n, b, rows, dst, dev))) return rc;
+  const bool limits = !(flags & IK_F_NO_LIMITS);
+  rc = sharded_run(c, IK_METHOD_FABRIK, P, R, nreg, dfk, [&](const PartJob &j) {
+    return fabrik_launch(c, dp + 3 * j.b, j.m, tol, max_iter, reinterpret_cast<double *>(j.at[0]),
+                         iters ? reinterpret_cast<int32_t *>(j.at[1]) : nullptr, nullptr,
+                         j.fk_err, limits, work, j.S);
+  });
+  if (rc) return rc;
+  if (!dev) {
+    char *ho[2] = {reinterpret_cast<char *>(ang), reinterpret_cast<char *>(iters)};
+    if ((rc = host_results_out(c, P, R, nreg, ho, hs.fk, fk_err))) return rc;
+  }
   if (flags & IK_F_ASYNC) return IK_OK;
   return sharded_stats(c, stats);
 }

@@ -2,26 +2,30 @@
 
 The reference "scales" by running competing-consumer RPC workers, one message
 at a time (rpc_broker.py:55-104, README.md:11).  Here every point is
-independent, so one batch is split into contiguous shards (rank r owns
-[floor(r N / g), floor((r+1) N / g)), ik_shard_range), each rank solves its
-shard on its own GPU, and ONE all-gather inside the library
-(ik_*_solve_sharded) delivers every rank's result rows plus a tail record of
-its stats, so every rank ends with the whole batch and the whole batch's stats
-(the lowest global failing index -- the reference's sequential exception
-precedence -- iteration sums, FK-error max/sum) without any other collective.
+independent, so one batch is split over the ranks in C chunks of g parts (rank r
+owns rows [(c g + r) S, (c g + r + 1) S) of chunk c, S = ceil(n / (C g)),
+ik_shard_plan_of / ik_shard_part), each rank solves its parts on its own GPU
+straight into their global rows of the output arrays, and the library
+all-gathers every chunk IN PLACE while the next one is solved
+(ik_*_solve_sharded).  Every rank ends with the whole batch's angles (and
+FABRIK iteration counts) and, from a tail record that rides with the last
+chunk, the whole batch's stats -- the lowest global failing index (the
+reference's sequential exception precedence), iteration sums, FK-error
+max / sum / histogram -- without any other collective.  Per-point FK errors
+stay on their rank.
 
 torch.distributed is only the control plane here: it hands rank 0's RCCL
 unique id to the other ranks (and gives bench.py its barrier); the data path
 is the library's communicator, as a C-ABI caller without torch would use it
 (INTEGRATION.md).
 
-The host-side mirror of the gather protocol (pack_block / unpack_blocks, the
-library's layout and tail records) is what the library does on the device and
-in its host-pointer path; the CPU tests drive it over gloo with world size 2.
+The host-side mirror of the protocol (plan_of / part_bounds and
+gather_in_place, the library's split and its in-place chunk gathers with the
+ragged last chunk staged) is what the library does on the device; the CPU tests
+drive it over gloo with world sizes 2 and 3.
 """
 from __future__ import annotations
 
-import ctypes
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -29,9 +33,26 @@ import numpy as np
 from . import _native
 
 
+def plan_of(n: int, world: int, chunks: int = 1) -> Tuple[int, int, int]:
+    """(chunks holding rows, part rows S, rows of the full chunks) = ik_shard_plan_of."""
+    cg = chunks * world
+    S = -(-n // cg) if n > 0 else 0
+    per = S * world
+    C = -(-n // per) if n > 0 else 0
+    full = (n // per) * per if per > 0 else 0
+    return C, S, full
+
+
+def part_bounds(n: int, world: int, chunks: int, rank: int, chunk: int) -> Tuple[int, int]:
+    """Rank's rows [begin, end) of chunk `chunk` (= ik_shard_part)."""
+    _, S, _ = plan_of(n, world, chunks)
+    lo = (chunk * world + rank) * S
+    return min(lo, n), min(lo + S, n)
+
+
 def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
-    """Rank's rows [begin, end) of an n-point batch (= ik_shard_range)."""
-    return (n * rank) // world, (n * (rank + 1)) // world
+    """Rank's rows [begin, end) of an n-point batch in one chunk (= ik_shard_range)."""
+    return part_bounds(n, world, 1, rank, 0)
 
 
 def exchange_unique_id(rank: int, broadcast: Callable[[Optional[bytes]], bytes]) -> bytes:
@@ -53,7 +74,7 @@ class ShardedContext:
     """A libikhip context bound to an RCCL communicator of `world` ranks.
     ann / fabrik take the WHOLE batch on every rank (host numpy arrays, or
     device tensors via the *_device methods) and return the whole batch's
-    results and stats."""
+    results and stats (fk_err: this rank's rows only)."""
 
     def __init__(self, ctx: _native.Context, world: int, rank: int, uid: bytes):
         self.ctx = ctx
@@ -63,6 +84,16 @@ class ShardedContext:
 
     def close(self):
         self.ctx.comm_destroy()
+
+    def info(self):
+        """(ranks, rank, chunks of the last call) as the library holds them."""
+        return self.ctx.comm_info()
+
+    def set_chunks(self, chunks: int):
+        self.ctx.comm_set_chunks(chunks)
+
+    def fk_err_quantile(self, q: float) -> float:
+        return self.ctx.fk_err_quantile(q)
 
     def ann(self, pts, check_limits=True, want_fk_err=False):
         return self.ctx.ann_solve_sharded(pts, check_limits, want_fk_err)
@@ -91,38 +122,59 @@ def init_from_env(ctx: _native.Context) -> ShardedContext:
     return ShardedContext(ctx, world, rank, uid)
 
 
-# ---- host mirror of the gather protocol ------------------------------------------
-def pack_block(layout: _native.GatherLayout, regions: Sequence[np.ndarray],
-               tail: _native.ShardTail) -> np.ndarray:
-    """One rank's block of the all-gather (uint8): region q's rows at offset[q],
-    then the tail record, as the library lays it out in its send buffer."""
-    blk = np.zeros(layout.block_bytes, np.uint8)
-    for q, arr in enumerate(regions):
-        raw = np.ascontiguousarray(arr).view(np.uint8).reshape(-1)
-        if raw.size > layout.shard * layout.row_bytes[q]:
-            raise ValueError(f"region {q}: {raw.size} bytes exceed the layout's shard")
-        blk[layout.offset[q]: layout.offset[q] + raw.size] = raw
-    tb = np.frombuffer(bytes(tail), np.uint8)
-    blk[layout.tail_offset: layout.tail_offset + tb.size] = tb
-    return blk
+# ---- host mirror of the protocol ---------------------------------------------
+def fkhist(err: np.ndarray) -> np.ndarray:
+    """A rank's FK-error histogram (IK_FKHIST_BINS uint32), numpy restatement of
+    fkhist_bin: 16 bins per octave from the float64 exponent and top 4 mantissa
+    bits; NaN / inf / negative values are not counted."""
+    e = np.asarray(err, np.float64).reshape(-1)
+    e = e[np.isfinite(e) & (e >= 0)]
+    bits = np.abs(e).view(np.uint64)
+    k = ((bits >> np.uint64(52)).astype(np.int64) - (1023 - 64)) * 16 + \
+        ((bits >> np.uint64(48)) & np.uint64(15)).astype(np.int64)
+    k = np.clip(k, 0, _native.IK_FKHIST_BINS - 1)
+    return np.bincount(k, minlength=_native.IK_FKHIST_BINS).astype(np.uint32)
 
 
-def unpack_blocks(layout: _native.GatherLayout, blocks: np.ndarray, n: int,
-                  dtypes: Sequence[np.dtype], widths: Sequence[int]):
-    """Every rank's block (world x block_bytes uint8) -> each region's rows of the
-    whole batch in point order, and the tails (what the library's unpack kernel
-    and per-rank D2H copies do)."""
-    world = blocks.shape[0]
-    outs: List[np.ndarray] = [np.empty((n, w), dt) for dt, w in zip(dtypes, widths)]
-    tails = []
-    for r in range(world):
-        lo, hi = shard_bounds(n, world, r)
-        for q, out in enumerate(outs):
-            rb = layout.row_bytes[q]
-            raw = blocks[r, layout.offset[q]: layout.offset[q] + (hi - lo) * rb]
-            out[lo:hi] = raw.view(out.dtype).reshape(hi - lo, out.shape[1])
-        t = _native.ShardTail()
-        ctypes.memmove(ctypes.addressof(t),
-                       blocks[r, layout.tail_offset:].ctypes.data, ctypes.sizeof(t))
-        tails.append(t)
-    return outs, tails
+def hist_quantile(hists: Sequence[np.ndarray], q: float) -> float:
+    """ik_fk_err_quantile from gathered histograms: the upper edge of the bin
+    holding the ceil(q m)-th smallest of the m counted errors."""
+    h = np.sum(np.stack([np.asarray(x, np.uint64) for x in hists]), axis=0)
+    tot = int(h.sum())
+    if tot == 0:
+        return float("nan")
+    want = max(1, int(np.ceil(q * tot)))
+    b = int(np.searchsorted(np.cumsum(h), want))
+    if b >= _native.IK_FKHIST_BINS - 1:
+        return float("inf")
+    return float(np.ldexp(1.0 + (b % 16 + 1) / 16.0, b // 16 - 64))
+
+
+def gather_in_place(n: int, world: int, rank: int, chunks: int,
+                    solve_part: Callable[[int, int], Sequence[np.ndarray]],
+                    outs: List[np.ndarray], all_gather: Callable[[np.ndarray, np.ndarray], None]):
+    """The library's sharded call on host arrays: for every chunk, solve_part(b,
+    e) gives this rank's rows of each gathered output, written at their global
+    rows (or, in the ragged last chunk, at rank offset r S of a g S-row stage),
+    then all_gather(send, recv) fills in every rank's rows in place -- recv is
+    the chunk's g S rows and send the rank's S of them, as ncclAllGather's
+    in-place mode.  Returns this rank's parts [(b, e)]."""
+    C, S, _ = plan_of(n, world, chunks)
+    parts = []
+    for c in range(C):
+        b, e = part_bounds(n, world, chunks, rank, c)
+        cb = c * world * S
+        staged = cb + world * S > n
+        rows = solve_part(b, e) if e > b else [np.zeros((0,) + o.shape[1:], o.dtype)
+                                                for o in outs]
+        for out, r in zip(outs, rows):
+            if staged:
+                st = np.zeros((world * S,) + out.shape[1:], out.dtype)
+                st[rank * S: rank * S + (e - b)] = r
+                all_gather(st[rank * S:(rank + 1) * S], st)
+                out[cb:n] = st[:n - cb]
+            else:
+                out[b:e] = r
+                all_gather(out[b:e], out[cb:cb + world * S])
+        parts.append((b, e))
+    return parts

@@ -8,7 +8,10 @@ Model files (ann.py:78-95):
   * `<name>.h5` (Keras HDF5, read by models/keras_h5.py without h5py) with the
     reference's `<name>_scaler_x.bin` / `<name>_scaler_y.bin` beside it
     (decoded by models/scaler_bin.py without unpickling);
-  * `<name>.npz` written by save_model() (weights, activations and scalers).
+  * save_model() writes that same layout (`<prefix>_<timestamp>.h5` through
+    models/hdf5_write.py, the scalers as joblib-dumped sklearn StandardScalers)
+    so the reference's load_model can open it; `<name>.npz` (weights,
+    activations and scalers) is also read.
 Training (ann.py:27-68) is out of scope for this engine.
 """
 from __future__ import annotations
@@ -174,8 +177,13 @@ class ANN:
         return self.model
 
     def save_model(self, prefix='model'):
-        """Save model to `<prefix>_<timestamp>.npz` (weights + scalers)."""
+        """Save model to `<prefix>_<timestamp>.h5` plus `..._scaler_x.bin` /
+        `..._scaler_y.bin` (ann.py:87-95); returns the .h5 path."""
+        from ..models.keras_h5 import save_keras_dense_model
+        from ..models.scaler_bin import save_scaler
         timestamp_str = str(datetime.timestamp(datetime.now())).replace('.', '-')
-        path = f'{prefix}_{timestamp_str}.npz'
-        save_npz_model(path, self.model, self.x_data_skaler, self.y_data_skaler)
-        return path
+        base = f'{prefix}_{timestamp_str}'
+        save_keras_dense_model(f'{base}.h5', self.model)
+        save_scaler(f'{base}_scaler_x.bin', self.x_data_skaler)
+        save_scaler(f'{base}_scaler_y.bin', self.y_data_skaler)
+        return f'{base}.h5'

@@ -26,8 +26,8 @@ class ForwardKinematics:
         self.thetas, self.epsilons, self.ais, self.alphas = self.dh_matrix
         self.no_of_features = len(self.thetas)
         assert self.no_of_features >= 3
-        if self.no_of_features > 8:
-            raise NotImplementedError('the HIP FK kernels take DH chains of 3 to 8 joints')
+        if self.no_of_features > 1024:
+            raise NotImplementedError('the HIP FK kernels take DH chains of 3 to 1024 joints')
 
     def _ctx(self):
         """The process context with this object's DH table; the link lengths and

@@ -68,3 +68,48 @@ def load_keras_dense_model(path: str):
         if Ws[i].shape[0] != Ws[i - 1].shape[1]:
             raise Hdf5Error(f"{path}: layer {lnames[i]} input width mismatch")
     return DenseModel(Ws, bs, acts, name=path, layer_names=lnames)
+
+
+def _dense_config(name: str, units: int, act: str) -> dict:
+    return {"name": name, "trainable": True, "dtype": "float32", "units": int(units),
+            "activation": act, "use_bias": True,
+            "kernel_initializer": {"class_name": "GlorotUniform", "config": {"seed": None}},
+            "bias_initializer": {"class_name": "Zeros", "config": {}},
+            "kernel_regularizer": None, "bias_regularizer": None,
+            "activity_regularizer": None, "kernel_constraint": None, "bias_constraint": None}
+
+
+def save_keras_dense_model(path: str, model, keras_version: str = "2.11.0"):
+    """Write `model` (a DenseModel) as Keras' model.save('*.h5') lays out a
+    Sequential of Dense layers (ann.py:46-56,92): root attributes backend /
+    keras_version / model_config (JSON), `model_weights` with `layer_names`, one
+    group per layer with `weight_names` and the float32 datasets at
+    `<layer>/<layer>/kernel:0` and `bias:0`.  No h5py: models/hdf5_write.py."""
+    from . import hdf5_write as W
+    dims = model.dims
+    names = (list(model.layer_names) if len(model.layer_names) == len(model.weights)
+             and len(set(model.layer_names)) == len(model.weights)
+             and all(n and "/" not in n for n in model.layer_names)
+             else ["dense"] + [f"dense_{i}" for i in range(1, len(model.weights))])
+    layers = [{"class_name": "InputLayer",
+               "config": {"batch_input_shape": [None, int(dims[0])], "dtype": "float32",
+                          "sparse": False, "ragged": False, "name": "input_1"}}]
+    layers += [{"class_name": "Dense", "config": _dense_config(nm, dims[i + 1], act)}
+               for i, (nm, act) in enumerate(zip(names, model.activations))]
+    cfg = {"class_name": "Sequential", "config": {"name": "sequential", "layers": layers}}
+    root = W.Group()
+    root.attrs["backend"] = "tensorflow"
+    root.attrs["keras_version"] = keras_version
+    root.attrs["model_config"] = json.dumps(cfg)
+    mw = root.group("model_weights")
+    mw.attrs["backend"] = "tensorflow"
+    mw.attrs["keras_version"] = keras_version
+    mw.attrs["layer_names"] = names
+    for nm, w, b in zip(names, model.weights, model.biases):
+        g = mw.group(nm)
+        wn = [f"{nm}/kernel:0", f"{nm}/bias:0"]
+        g.attrs["weight_names"] = wn
+        g.dataset(wn[0], np.asarray(w, np.float32))
+        g.dataset(wn[1], np.asarray(b, np.float32).reshape(-1))
+    W.write(path, root)
+    return path

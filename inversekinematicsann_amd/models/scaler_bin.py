@@ -240,7 +240,11 @@ def parse_joblib_pickle(data: bytes):
             if isinstance(obj, _Obj):
                 obj.state = state
                 if obj.func == ("global", "joblib.numpy_pickle", "NumpyArrayWrapper"):
-                    # the array bytes follow the BUILD opcode in the stream
+                    # the array bytes follow the BUILD opcode in the stream;
+                    # joblib >= 1.2 aligns them: one byte of padding length,
+                    # then that many pad bytes (numpy_array_alignment_bytes)
+                    if state.get("numpy_array_alignment_bytes") is not None:
+                        take(u8())
                     dt = _dtype_of(state["dtype"])
                     shape = tuple(state["shape"])
                     count = int(np.prod(shape)) if shape else 1
@@ -281,3 +285,24 @@ def save_scaler_npz(path: str, sc: ScalerParams):
     np.savez(path, mean=sc.mean, scale=sc.scale,
              var=sc.var if sc.var is not None else np.zeros(0),
              with_mean=np.bool_(sc.with_mean), with_std=np.bool_(sc.with_std))
+
+
+def save_scaler(path: str, sc: ScalerParams):
+    """Write a scaler as the reference does (ann.py:94-95: joblib.dump of a
+    fitted sklearn StandardScaler, compress=True), so that the reference's
+    load_model and load_scaler above both read it.  Needs joblib and
+    scikit-learn (writing only: nothing is unpickled here)."""
+    try:
+        import joblib
+        from sklearn.preprocessing import StandardScaler
+    except ImportError as e:  # pragma: no cover - both ship in this image
+        raise RuntimeError("saving a .bin scaler needs joblib and scikit-learn") from e
+    s = StandardScaler(with_mean=bool(sc.with_mean), with_std=bool(sc.with_std))
+    s.mean_ = np.asarray(sc.mean, np.float64).copy()
+    s.scale_ = np.asarray(sc.scale, np.float64).copy()
+    s.var_ = (np.asarray(sc.var, np.float64).copy() if sc.var is not None
+              else s.scale_ ** 2)
+    s.n_features_in_ = int(s.mean_.shape[0])
+    s.n_samples_seen_ = np.int64(sc.n_samples_seen if sc.n_samples_seen is not None else 0)
+    joblib.dump(s, path, compress=True)
+    return path

@@ -44,3 +44,43 @@ def test_ann_cpu_baseline_parity_fields():
     r = bench.cpu_baseline("ann", _Args(), sample_pts=pts,
                            gpu_out={"ang": ref.astype(np.float32)})
     assert r["parity"]["ok"] and r["parity"]["max_abs_diff_vs_oracle_fp32"] <= 1e-6
+
+
+def test_launch_command_for_n_gpus():
+    """`bench.py --gpus 8` runs 8 ranks itself through torch.distributed.run on
+    127.0.0.1, passing its own arguments through (the driver calls
+    `python3 bench.py --gpus N` with no launcher)."""
+    import bench
+    argv = ["--gpus", "8", "--steps", "5", "--warmup", "1"]
+    cmd = bench.launch_command(argv, 8, 29511)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and "--master-port=29511" in cmd
+    assert cmd[-len(argv) - 1] == os.path.join(ROOT, "bench.py") and cmd[-len(argv):] == argv
+    assert bench._gpus_arg(["--gpus=4"]) == 4 and bench._gpus_arg([]) == 1
+
+
+def test_maybe_launch_spawns_child_not_exec(monkeypatch):
+    import subprocess
+    import bench
+    seen = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(subprocess, "call", lambda cmd, env=None: seen.append((cmd, env)) or 3)
+    assert bench.maybe_launch(["--gpus", "2", "--gather", "0"]) == 3  # the child's exit code
+    (cmd, env), = seen
+    assert "--nproc-per-node=2" in cmd and cmd[-3:] == ["--gpus", "2", "--gather", "0"][-3:]
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+    assert bench.maybe_launch(["--gpus", "1"]) is None  # N = 1: this process is the bench
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.maybe_launch(["--gpus", "2"]) is None  # already a rank
+    assert len(seen) == 1
+
+
+def test_rank_count_mismatch_exits_nonzero():
+    """A rank whose WORLD_SIZE differs from --gpus never prints a line."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and p.stdout == ""
+    assert "--gpus 8 but 1 rank" in p.stderr

@@ -12,8 +12,8 @@ from tests.conftest import GOLDEN, ROOT
 def _declared_symbols():
     with open(os.path.join(ROOT, "include", "ikhip.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char \*|void \*)\s*(ik_\w+)\s*\(", src,
-                                 re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|double|const char \*|void \*)\s*(ik_\w+)\s*\(",
+                                 src, re.M)))
 
 
 def test_header_matches_binding_list():

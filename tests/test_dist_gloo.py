@@ -1,11 +1,12 @@
-"""world_size-2 (and 3) gloo tests of the sharded solve's gather protocol on the
-CPU: the library's own shard split (ik_shard_range), block layout
-(ik_gather_layout_of) and tail reduction (ik_tail_reduce), with every rank's
-block built from its shard's solve and one all_gather of the blocks -- the
-library's RCCL path with gloo as the transport.  The per-rank solver is the C
-oracle (test infrastructure, the checker's stand-in for the GPU solve); the
-gathered rows and the reduced stats must equal one single-process solve of the
-whole batch bit for bit."""
+"""world_size-2 (and 3) gloo tests of the sharded solve's protocol on the CPU:
+the library's own split in chunks (ik_shard_plan_of / ik_shard_part), its
+in-place chunk all-gathers with the ragged last chunk staged (dist.gather_in_place,
+the host mirror of ik_shard.hip's sharded_run), the tail reduction
+(ik_tail_reduce) and the FK-error histograms (ik_fkhist_bin, quantiles), with
+gloo as the transport.  The per-rank solver is the C oracle (test
+infrastructure, the checker's stand-in for the GPU solve); the gathered rows and
+the reduced stats must equal one single-process solve of the whole batch bit for
+bit."""
 import os
 import socket
 
@@ -22,34 +23,51 @@ def _free_port():
     return p
 
 
-def _shard_solve(local, lo, tol, mi):
-    """One rank's shard through the oracle: the rows and the tail record the
-    library's pack_tail_kernel would write (global indices)."""
-    from inversekinematicsann_amd import _native
+def _part_solve(pts, b, e, tol, mi):
+    """Rows [b, e) through the oracle: angles, iterations, FK errors, and the
+    stats the library's pack_tail_kernel would record (global indices)."""
     from oracle import oracle as O
+    local = pts[b:e]
     ang, it, _, st = O.fabrik_ikine(local, tol, mi)
-    xyz, _, fst = O.fk(np.nan_to_num(ang))
+    xyz, _, _ = O.fk(np.nan_to_num(ang))
     err = np.sqrt(((xyz - local) ** 2).sum(axis=1))
     err[st != 0] = np.nan
-    t = _native.ShardTail()
     oob = O.check_limits(local)
-    t.first_oob = lo + oob if oob >= 0 else -1
     bad = np.nonzero(st)[0]
-    t.first_err = lo + int(bad[0]) if len(bad) else -1
-    t.first_err_code = int(st[bad[0]]) if len(bad) else 0
-    t.max_iters = int(it.max()) if len(it) else 0
-    t.sum_iters = int(it.sum())
-    t.n_capped = int((it >= mi).sum())
     fin = err[np.isfinite(err)]
-    t.max_fk_err = float(fin.max()) if len(fin) else 0.0
-    t.sum_fk_err = float(fin.sum())
-    t.rows = len(local)
-    return ang, it, err, t
+    stats = dict(first_oob=b + oob if oob >= 0 else -1,
+                 first_err=b + int(bad[0]) if len(bad) else -1,
+                 first_err_code=int(st[bad[0]]) if len(bad) else 0,
+                 max_iters=int(it.max()) if len(it) else 0, sum_iters=int(it.sum()),
+                 n_capped=int((it >= mi).sum()),
+                 max_fk_err=float(fin.max()) if len(fin) else 0.0, sum_fk_err=float(fin.sum()),
+                 rows=len(local))
+    return ang, it, err, stats
 
 
-def _worker(rank, world, port, n, bad, q):
+def _tail(parts_stats):
+    """The rank's tail from its parts' stats in chunk order (pack_tail_kernel)."""
+    from inversekinematicsann_amd import _native
+    t = _native.ShardTail()
+    t.first_oob = t.first_err = -1
+    for s in parts_stats:
+        if t.first_oob < 0 and s["first_oob"] >= 0:
+            t.first_oob = s["first_oob"]
+        if t.first_err < 0 and s["first_err"] >= 0:
+            t.first_err, t.first_err_code = s["first_err"], s["first_err_code"]
+        t.max_iters = max(t.max_iters, s["max_iters"])
+        t.sum_iters += s["sum_iters"]
+        t.n_capped += s["n_capped"]
+        t.max_fk_err = max(t.max_fk_err, s["max_fk_err"])
+        t.sum_fk_err += s["sum_fk_err"]
+        t.rows += s["rows"]
+    return t
+
+
+def _worker(rank, world, port, n, chunks, bad, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
+    import ctypes
     import torch
     import torch.distributed as dist
     from inversekinematicsann_amd import _native
@@ -60,30 +78,57 @@ def _worker(rank, world, port, n, bad, q):
         pts = random_dist(n, seed=11)
         for i, v in bad:
             pts[i] = v
-        lo, hi = _native.shard_range(n, world, rank)
-        assert (lo, hi) == D.shard_bounds(n, world, rank)
-        L = _native.gather_layout(_native.IK_METHOD_FABRIK, n, world, True, True)
-        ang, it, err, tail = _shard_solve(pts[lo:hi], lo, 1e-3, 100)
-        blk = D.pack_block(L, [ang, it, err], tail)
-        out = [torch.empty(L.block_bytes, dtype=torch.uint8) for _ in range(world)]
-        dist.all_gather(out, torch.from_numpy(blk))  # the one collective
-        blocks = np.stack([o.numpy() for o in out])
-        (g_ang, g_it, g_err), tails = D.unpack_blocks(L, blocks, n,
-                                                      [np.float64, np.int32, np.float64],
-                                                      [4, 1, 1])
+        plan = _native.shard_plan(n, world, chunks)
+        assert (plan.chunks, plan.part_rows, plan.full_rows) == D.plan_of(n, world, chunks)
+        ang = np.full((n, 4), -7.0)
+        it = np.full(n, -7, np.int32)
+        err = np.full(n, -7.0)  # only this rank's rows are written (stays local)
+        stats = []
+
+        def solve_part(b, e):
+            assert (b, e) == _native.shard_part(plan, rank, len(stats))
+            a, i, f, s = _part_solve(pts, b, e, 1e-3, 100)
+            err[b:e] = f
+            stats.append(s)
+            return [a, i]
+
+        def all_gather(send, recv):  # ncclAllGather in place: recv = g x len(send)
+            out = list(torch.from_numpy(np.ascontiguousarray(recv)).chunk(world))
+            dist.all_gather(out, torch.from_numpy(np.ascontiguousarray(send)))
+            recv[...] = torch.cat(out).numpy()
+
+        parts = D.gather_in_place(n, world, rank, chunks, solve_part, [ang, it], all_gather)
+        assert len(parts) == plan.chunks
+        while len(stats) < len(parts):  # empty parts record zero stats
+            stats.append(dict(first_oob=-1, first_err=-1, first_err_code=0, max_iters=0,
+                              sum_iters=0, n_capped=0, max_fk_err=0.0, sum_fk_err=0.0, rows=0))
+        # the tail block (stats record + histogram), one all-gather with the last chunk
+        tb = np.concatenate([np.frombuffer(bytes(_tail(stats)), np.uint8),
+                             D.fkhist(err[[i for b, e in parts for i in range(b, e)]])
+                             .view(np.uint8)])
+        blocks = [torch.empty(tb.size, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(blocks, torch.from_numpy(tb))
+        tails, hists = [], []
+        for blk in blocks:
+            raw = blk.numpy()
+            t = _native.ShardTail()
+            ctypes.memmove(ctypes.addressof(t), raw[:64].ctypes.data, 64)
+            tails.append(t)
+            hists.append(raw[64:].view(np.uint32))
         st = _native.tail_reduce(tails)
-        q.put((rank, g_ang, g_it[:, 0], g_err[:, 0], st.as_dict()))
+        q.put((rank, ang, it, err, st.as_dict(), D.hist_quantile(hists, 0.99), parts))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001 -- reported to the parent
-        q.put((rank, repr(e)))
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc()))
 
 
-def _run(world, n, bad=()):
+def _run(world, n, chunks=1, bad=()):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, list(bad), q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, chunks, list(bad), q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -92,69 +137,103 @@ def _run(world, n, bad=()):
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in res:
-        assert len(r) == 5, r
+        assert len(r) == 7, r
     return sorted(res, key=lambda r: r[0])
 
 
-def test_shard_bounds_match_library():
+def test_plan_matches_library_and_covers_batch():
     from inversekinematicsann_amd import _native
-    from inversekinematicsann_amd.dist import shard_bounds
-    for n in (0, 1, 7, 1000, 1_000_001, 10_000_000):
-        for w in (1, 2, 3, 8):
-            b = [shard_bounds(n, w, r) for r in range(w)]
-            assert b[0][0] == 0 and b[-1][1] == n
-            assert all(b[i][1] == b[i + 1][0] for i in range(w - 1))
-            assert b == [_native.shard_range(n, w, r) for r in range(w)]
+    from inversekinematicsann_amd import dist as D
+    for n in (0, 1, 2, 7, 64, 1000, 1001, 99_991, 1_000_000, 10_000_000):
+        for w in (1, 2, 3, 5, 8):
+            for c in (1, 2, 3, 4, 8):
+                p = _native.shard_plan(n, w, c)
+                assert (p.n, p.nranks) == (n, w)
+                assert (p.chunks, p.part_rows, p.full_rows) == D.plan_of(n, w, c)
+                assert p.chunks <= c
+                rows = np.zeros(n, np.int32)
+                for k in range(p.chunks):
+                    cb = k * w * p.part_rows
+                    for r in range(w):
+                        b, e = _native.shard_part(p, r, k)
+                        assert (b, e) == D.part_bounds(n, w, c, r, k)
+                        # in-place layout: the part sits at rank offset r S of its chunk
+                        assert b == min(cb + r * p.part_rows, n) and e - b <= p.part_rows
+                        rows[b:e] += 1
+                    # only the last chunk may be ragged (staged)
+                    assert (cb + w * p.part_rows <= n) == (k < p.chunks - 1 or p.full_rows == n)
+                assert (rows == 1).all()
+                assert p.full_rows == n or p.full_rows == (p.chunks - 1) * w * p.part_rows
+                # one chunk: ik_shard_range
+                if c == 1:
+                    for r in range(w):
+                        assert _native.shard_range(n, w, r) == D.shard_bounds(n, w, r) == \
+                            _native.shard_part(p, r, 0)
 
 
-def test_gather_layout():
+def test_fkhist_bins_match_library():
     from inversekinematicsann_amd import _native
-    L = _native.gather_layout(_native.IK_METHOD_FABRIK, 10, 3, True, True)
-    assert L.shard == 4 and L.nregion == 3
-    assert list(L.row_bytes) == [32, 4, 8]
-    assert list(L.offset) == [0, 128, 192] and L.tail_offset == 256 and L.block_bytes == 320
-    L = _native.gather_layout(_native.IK_METHOD_ANN, 1_000_000, 8)
-    assert L.nregion == 1 and L.row_bytes[0] == 16 and L.block_bytes == 125_000 * 16 + 64
+    from inversekinematicsann_amd import dist as D
+    rng = np.random.default_rng(0)
+    vals = np.concatenate([
+        [0.0, -0.0, 5e-324, 2.0 ** -64, 2.0 ** -65, 1.0, 1.0625, 1.0624999, 2.0 ** 63,
+         2.0 ** 64, 1e300, np.inf, -1.0, np.nan],
+        10.0 ** rng.uniform(-20, 3, 2000)])
+    for v in vals:
+        b = _native.fkhist_bin(v)
+        h = D.fkhist(np.array([v]))
+        if b < 0:
+            assert h.sum() == 0, v
+        else:
+            assert h[b] == 1 and h.sum() == 1, v
+            # monotonic bins: v lies below the bin's upper edge
+            assert v < _native.fkhist_upper(b) or b == _native.IK_FKHIST_BINS - 1
+            if b > 0:
+                assert v >= _native.fkhist_upper(b - 1)
+    # quantile: an upper bound within 1/16 octave of the exact order statistic
+    e = 10.0 ** rng.uniform(-12, 1, 100_000)
+    for q in (0.5, 0.9, 0.99, 1.0):
+        exact = np.sort(e)[int(np.ceil(q * e.size)) - 1]
+        got = D.hist_quantile([D.fkhist(e[:40_000]), D.fkhist(e[40_000:])], q)
+        assert exact <= got <= exact * 2 ** (1 / 16) * (1 + 1e-12), (q, exact, got)
 
 
-@pytest.mark.parametrize("world,n", [(2, 1001), (2, 64), (3, 1000), (2, 1), (3, 2)])
-def test_gather_matches_single_process(world, n):
+@pytest.mark.parametrize("world,n,chunks", [(2, 1001, 1), (2, 64, 1), (3, 1000, 1), (2, 1, 1),
+                                            (3, 2, 1), (2, 1001, 4), (3, 1000, 3), (2, 12, 4)])
+def test_gather_matches_single_process(world, n, chunks):
+    from inversekinematicsann_amd import dist as D
     from inversekinematicsann_amd.robot.position_generator import random_dist
     pts = random_dist(n, seed=11)
-    ref_ang, ref_it, ref_err, ref_t = _shard_solve(pts, 0, 1e-3, 100)
-    for rank, ang, it, err, st in _run(world, n):
-        # every rank holds the whole batch, bit for bit
+    ref_ang, ref_it, ref_err, ref_t = _part_solve(pts, 0, n, 1e-3, 100)
+    seen = np.zeros(n, np.int32)
+    for rank, ang, it, err, st, p99, parts in _run(world, n, chunks):
+        # every rank holds the whole batch's gathered rows, bit for bit
         assert np.array_equal(ang, ref_ang) and np.array_equal(it, ref_it)
-        assert np.array_equal(err, ref_err, equal_nan=True)
+        # FK errors: only this rank's own rows, equal to the one-process ones
+        mine = np.zeros(n, bool)
+        for b, e in parts:
+            mine[b:e] = True
+            seen[b:e] += 1
+        assert np.array_equal(err[mine], ref_err[mine], equal_nan=True)
+        assert (err[~mine] == -7.0).all()
         assert st["first_oob"] == -1 and st["first_err"] == -1
-        assert st["sum_iters"] == ref_t.sum_iters and st["max_iters"] == ref_t.max_iters
-        assert st["n_capped"] == ref_t.n_capped
-        assert st["max_fk_err"] == ref_t.max_fk_err
+        assert st["sum_iters"] == ref_t["sum_iters"] and st["max_iters"] == ref_t["max_iters"]
+        assert st["n_capped"] == ref_t["n_capped"]
+        assert st["max_fk_err"] == ref_t["max_fk_err"]
         # per-rank partial sums in rank order vs one sum: equal up to rounding
-        assert abs(st["sum_fk_err"] - ref_t.sum_fk_err) <= 1e-12 * max(1.0, ref_t.sum_fk_err)
+        assert abs(st["sum_fk_err"] - ref_t["sum_fk_err"]) <= 1e-12 * max(1.0, ref_t["sum_fk_err"])
+        assert p99 == D.hist_quantile([D.fkhist(ref_err)], 0.99)
+    assert (seen == 1).all()  # the ranks' parts cover the batch once
 
 
 def test_lowest_failing_index_across_shards():
     # an out-of-reach point on rank 1 and ZeroDivision points on both ranks: the
     # reduced stats carry the lowest GLOBAL index of each (inverse.py:117, point.py:40)
     n = 100
-    res = _run(2, n, bad=[(70, [1.0, 2.0, -4.0]), (10, [0.0, 0.0, 2.0]), (80, [0.0, 0.0, 2.0])])
-    for _, ang, _, err, st in res:
-        assert st["first_oob"] == 70
-        assert st["first_err"] == 10 and st["first_err_code"] == 3
-        assert np.isnan(ang[10]).all() and np.isnan(err[80])
-
-
-def test_unpack_rank_formula():
-    """The device unpack kernel (ik_shard.hip gather_unpack_kernel) finds row i's
-    rank as ceil((i + 1) g / n) - 1 and its local row as i - floor(r n / g): the
-    same split as ik_shard_range for every row."""
-    from inversekinematicsann_amd.dist import shard_bounds
-    for n in (1, 2, 7, 64, 1000, 1001, 99_991):
-        for g in (1, 2, 3, 5, 8):
-            i = np.arange(n, dtype=np.int64)
-            r = ((i + 1) * g + n - 1) // n - 1
-            local = i - (n * r) // g
-            lo = np.array([shard_bounds(n, g, k)[0] for k in range(g)])
-            hi = np.array([shard_bounds(n, g, k)[1] for k in range(g)])
-            assert ((lo[r] <= i) & (i < hi[r])).all() and (local == i - lo[r]).all()
+    for chunks in (1, 3):
+        res = _run(2, n, chunks,
+                   bad=[(70, [1.0, 2.0, -4.0]), (10, [0.0, 0.0, 2.0]), (80, [0.0, 0.0, 2.0])])
+        for _, ang, _, err, st, _, _ in res:
+            assert st["first_oob"] == 70
+            assert st["first_err"] == 10 and st["first_err_code"] == 3
+            assert np.isnan(ang[10]).all() and np.isnan(ang[80]).all()

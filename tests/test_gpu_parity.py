@@ -607,10 +607,11 @@ def test_ann_tile_variants_agree(ctx1, tmp_path, mode):
     assert np.array_equal(mine, other["a"]) and np.array_equal(err, other["e"])
 
 
-@pytest.mark.parametrize("nj", [5, 6, 8])
+@pytest.mark.parametrize("nj", [5, 6, 8, 9, 13])
 def test_fk_chains_of_other_lengths(nj):
     """ForwardKinematics accepts any number of features >= 3 (forward.py:13-19):
-    5..8-joint DH tables on the GPU (ik_fk_chain) against the numpy restatement
+    5..8-joint DH tables (unrolled kernels) and 9 / 13 joints (the run-time joint
+    loop, fk_any_kernel) on the GPU (ik_fk_chain) against the numpy restatement
     of forward.py's nf x nf matrices (oracle.fk_n), and 3 features fail like
     the reference (IndexError, after the angle check)."""
     from inversekinematicsann_amd.kinematics.forward import ForwardKinematics

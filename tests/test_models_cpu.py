@@ -67,3 +67,67 @@ def test_train_model_is_out_of_scope():
     from inversekinematicsann_amd.kinematics.ann import ANN
     with pytest.raises(NotImplementedError):
         ANN({}, []).train_model(1, [], [])
+
+
+def test_hdf5_lookup3_known_values():
+    """The HDF5 metadata checksum: Jenkins lookup3 hashlittle's published values."""
+    from inversekinematicsann_amd.models.hdf5_write import lookup3
+    assert lookup3(b"") == 0xDEADBEEF
+    assert lookup3(b"Four score and seven years ago") == 0x17770551
+    assert lookup3(b"Four score and seven years ago", 1) == 0xCD628161
+
+
+def test_save_model_round_trip_h5_and_scalers(tmp_path):
+    """ANN.save_model writes the reference's layout (ann.py:87-95): <prefix>_<ts>.h5
+    in Keras' Sequential-of-Dense structure plus _scaler_{x,y}.bin joblib dumps of
+    sklearn StandardScalers; the h5py-free reader and the unpickling-free scaler
+    decoder read them back exactly, and joblib (the reference's loader) gives
+    working StandardScalers.  h5py (libhdf5) reads the .h5 where an interpreter
+    has it."""
+    import json
+    import subprocess
+    import joblib
+    from inversekinematicsann_amd.kinematics.ann import (ANN, REFERENCE_X_SCALER as XS,
+                                                         REFERENCE_Y_SCALER as YS, glorot_model)
+    from inversekinematicsann_amd.models.keras_h5 import load_keras_dense_model
+    from inversekinematicsann_amd.models.scaler_bin import load_scaler
+    a = ANN(None, None)
+    m = glorot_model((3, 40, 33, 4), seed=9, hidden_act="relu")
+    m.biases = [np.linspace(-1, 1, b.size).astype(np.float32) for b in m.biases]
+    a.set_model(m, XS, YS)
+    h5 = a.save_model(str(tmp_path / "roboarm_model"))
+    assert h5.startswith(str(tmp_path / "roboarm_model_")) and h5.endswith(".h5")
+    base = h5[:-3]
+    assert os.path.exists(base + "_scaler_x.bin") and os.path.exists(base + "_scaler_y.bin")
+    m2 = load_keras_dense_model(h5)
+    assert m2.activations == m.activations and m2.dims == m.dims
+    for w1, w2, b1, b2 in zip(m.weights, m2.weights, m.biases, m2.biases):
+        assert np.array_equal(w1, w2) and np.array_equal(b1, b2)
+    for sc, suf in ((XS, "x"), (YS, "y")):
+        got = load_scaler(f"{base}_scaler_{suf}.bin")
+        assert np.array_equal(got.mean, sc.mean) and np.array_equal(got.scale, sc.scale)
+        ref = joblib.load(f"{base}_scaler_{suf}.bin")  # a file this test wrote
+        x = np.arange(len(sc.mean), dtype=np.float64)[None, :] + 0.5
+        assert np.array_equal(ref.transform(x), (x - sc.mean) / sc.scale)
+    # the file loads into a new ANN like the reference's .h5 + .bin pair (ann.py:78-85)
+    b = ANN(None, None)
+    b.load_model(h5)
+    assert np.array_equal(b.x_data_skaler.mean, XS.mean)
+    py39 = "/opt/conda/bin/python3.9"
+    if os.path.exists(py39):
+        code = ("import h5py, json, numpy as np, sys\n"
+                "f = h5py.File(sys.argv[1], 'r')\n"
+                "cfg = json.loads(f.attrs['model_config'])\n"
+                "mw = f['model_weights']\n"
+                "out = {n.decode(): [np.asarray(mw[n][w]).tolist() for w in "
+                "mw[n].attrs['weight_names']] for n in mw.attrs['layer_names']}\n"
+                "print(json.dumps({'cfg': cfg, 'w': out}))\n")
+        r = subprocess.run([py39, "-c", code, h5], capture_output=True, text=True, timeout=120)
+        if r.returncode == 0 or "No module named 'h5py'" not in r.stderr:
+            assert r.returncode == 0, r.stderr[-2000:]
+            d = json.loads(r.stdout)
+            assert [L["class_name"] for L in d["cfg"]["config"]["layers"]] == \
+                ["InputLayer", "Dense", "Dense", "Dense"]
+            for i, nm in enumerate(m2.layer_names):
+                assert np.array_equal(np.asarray(d["w"][nm][0], np.float32), m.weights[i])
+                assert np.array_equal(np.asarray(d["w"][nm][1], np.float32), m.biases[i])
