@@ -398,6 +398,7 @@ def run_fabrik(job, args, tol=None, max_iter=None):
         res["gather_chunks"] = job.sc.info()[2]
         res["gather_ms"] = st.gather_ms
     mx, sm, sum_iters, n_capped = _stats_over_ranks(job, st, res)
+    res["cold"] = cold_steps(ctx, step)
     n = job.n_local
     res["mean_iters"] = sum_iters / job.total
     res["n_capped"] = int(n_capped)
@@ -499,6 +500,30 @@ def timed(ctx, step, args, world):
     ev_ms = ev0.elapsed_time(ev1) / args.steps
     return {"wall_s": wall, "ms_per_step": wall * 1e3 / args.steps, "event_ms_per_step": ev_ms,
             "kernels": kernels}
+
+
+def cold_steps(ctx, step, reps=3):
+    """The FABRIK step with the context's learned work order forgotten
+    (ik_fabrik_reset_order): the points go in point order, as on a fresh
+    context's first call (the CLI's and the RPC worker's first request), while
+    `value` is the warm steady state.  Median over `reps` (each cold call teaches
+    the table again, so each is preceded by a reset); scratch is already sized,
+    so this isolates the work order's effect."""
+    import torch
+    times = []
+    for _ in range(reps):
+        ctx.fabrik_reset_order()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        step()
+        e1.record()
+        torch.cuda.synchronize()
+        times.append(e0.elapsed_time(e1))
+    step()  # re-learn before anything else runs
+    torch.cuda.synchronize()
+    return {"ms": float(np.median(times)), "all_ms": times,
+            "note": "work-order table reset before each call (ik_fabrik_reset_order): point "
+                    "order, as a fresh context's first call; warm = ms_per_step"}
 
 
 def end_to_end(job, solve_host, args):
@@ -737,7 +762,7 @@ def main():
                                 "kernels_ms": r2["kernels"],
                                 **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
                                                       "mean_iters", "n_capped", "end_to_end",
-                                                      "gather_chunks", "gather_ms")
+                                                      "gather_chunks", "gather_ms", "cold")
                                    if k in r2}}
             cref = _config_ref("fabrik" if other.startswith("fabrik") else other, total, world,
                                1e-5 if other == "fabrik_tol1e-5" else args.tol,
@@ -776,7 +801,7 @@ def main():
         "kernels_ms": res["kernels"],
     }
     for k in ("max_fk_err", "mean_fk_err", "p99_fk_err", "fk_err_note", "mean_iters", "n_capped",
-              "end_to_end", "gather_ms"):
+              "end_to_end", "gather_ms", "cold"):
         if k in res:
             line[k] = res[k]
     if secondary:

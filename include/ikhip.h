@@ -123,6 +123,12 @@ int ik_fabrik_solve_fk(ik_ctx *ctx, const double *pts, int64_t n, double tol, in
                        double *ang, int32_t *iters, double *joints, double *fk_err, int flags,
                        ik_stats *stats);
 
+/* Forget the context's learned FABRIK work order (the per-goal-cell cost table
+ * the solves keep to start the hardest points first; DESIGN.md "Work order"):
+ * the next solve runs in point order, as a fresh context's first call does.
+ * Results never depend on it; only the launch's tail does. */
+int ik_fabrik_reset_order(ik_ctx *ctx);
+
 /* Fabrik.calculate, kinematics/fabrik.py:44-67, batched over n goals for a chain
  * of nj (2..8) joints: init is n x nj x 3 (or nj x 3 shared by all goals when
  * init_shared != 0), goals n x 3 -> joints n x nj x 3, iters n (nullable). */

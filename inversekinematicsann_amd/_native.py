@@ -32,7 +32,7 @@ ACTS = {"linear": 0, "tanh": 1, "relu": 2, "sigmoid": 3}
 
 EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_ctx_get_stream",
                     "ik_last_error", "ik_version", "ik_set_robot", "ik_check_limits", "ik_fk", "ik_fk_chain",
-                    "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_ann_load", "ik_ann_solve",
+                    "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_fabrik_reset_order", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode",
                     "ik_comm_unique_id", "ik_comm_init", "ik_comm_destroy", "ik_comm_info",
@@ -118,6 +118,7 @@ def load_library(path: str = LIB_PATH):
                                       st]
         L.ik_fabrik_solve_fk.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp, dp,
                                          ctypes.c_int, st]
+        L.ik_fabrik_reset_order.argtypes = [vp]
         L.ik_fabrik_calc.argtypes = [vp, ctypes.c_int, dp, dp, ctypes.c_int, dp, i64,
                                      ctypes.c_double, i32, dp, ip, ctypes.c_int, st]
         L.ik_ann_load.argtypes = [vp, ctypes.c_int, ip, ip, ctypes.POINTER(ctypes.c_void_p),
@@ -350,6 +351,11 @@ class Context:
             self.handle, args[0], n, float(tol), int(max_iter), args[1], args[2], args[3],
             args[4], flags, ctypes.byref(s))))
         return s
+
+    def fabrik_reset_order(self):
+        """Forget the learned FABRIK work order (ik_fabrik_reset_order): the next
+        solve starts cold, in point order, on the context's current stream."""
+        self._on_torch_stream(lambda: self._check(self.lib.ik_fabrik_reset_order(self.handle)))
 
     def fabrik_calc(self, dists, init, goals, tol=1e-3, max_iter=100):
         """Batched Fabrik.calculate; init n x nj x 3 or nj x 3 (shared)."""

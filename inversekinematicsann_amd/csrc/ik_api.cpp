@@ -498,6 +498,15 @@ int ik_fabrik_solve_fk(ik_ctx *c, const double *pts, int64_t n, double tol, int3
   return finish(c, flags, stats);
 }
 
+int ik_fabrik_reset_order(ik_ctx *c) {
+  if (!c) return fail(IK_E_BADARG, "ik_fabrik_reset_order: NULL context");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);  // ordered after the context's earlier calls, whatever their stream
+  IK_HIP(hipMemsetAsync(c->fab_ord, 0, sizeof(FabOrderDev), c->stream));
+  return IK_OK;
+}
+
 int ik_fabrik_calc(ik_ctx *c, int nj, const double *dists, const double *init,
                    int init_shared, const double *goals, int64_t n, double tol,
                    int32_t max_iter, double *joints, int32_t *iters, int flags,

@@ -125,19 +125,27 @@ class IkineRPCBroker:
     start = serve
 
     def close(self):
-        try:
-            self.channel.stop_consuming()
-        finally:
-            self.connection.close()
+        """Stop consuming and close; quiet when pika already closed the
+        connection (an interrupt can land in its I/O loop)."""
+        for step in (self.channel.stop_consuming, self.connection.close):
+            try:
+                step()
+            except Exception as e:  # noqa: BLE001 -- closing is best effort
+                log.debug("close: %s: %s", step.__name__, e)
 
 
 def main(argv: Optional[Sequence[str]] = None) -> int:
-    broker = IkineRPCBroker(get_ikine_engine_cli(argv))
+    """Start the broker; Ctrl+C at any point (model load, connect, serving) exits
+    cleanly with status 0, as the reference's main does (rpc_broker.py:107-119)."""
+    broker = None
     try:
+        broker = IkineRPCBroker(get_ikine_engine_cli(argv))
         broker.serve()
     except KeyboardInterrupt:
         log.info("interrupted; closing the connection")
-        broker.close()
+        print("CTRL+C interrupted")
+        if broker is not None:
+            broker.close()
     return 0
 
 

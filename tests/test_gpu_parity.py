@@ -379,6 +379,10 @@ def test_fabrik_work_order_is_invisible():
                 else:
                     assert np.array_equal(ang, first[0], equal_nan=True)
                     assert np.array_equal(it, first[1])
+        # a forgotten table (ik_fabrik_reset_order: point order again) changes nothing
+        c.fabrik_reset_order()
+        ang, it, _, _ = c.fabrik_solve(big, 1e-3, 100)
+        assert np.array_equal(ang, first[0], equal_nan=True) and np.array_equal(it, first[1])
         ref_ang, ref_it, _, _ = O.fabrik_ikine(big[:8192], 1e-3, 100)
         assert np.array_equal(first[1][:8192], ref_it)  # bit-exact iteration counts
         assert np.abs(first[0][:8192] - ref_ang).max() <= 1e-9

@@ -75,3 +75,26 @@ def test_engine_cli_and_broker_without_pika():
     except ImportError:
         with pytest.raises(RuntimeError, match="pika"):
             rpc_broker.IkineRPCBroker(eng)
+
+
+def test_ctrl_c_during_setup_and_close_errors(monkeypatch, capsys):
+    """Ctrl+C while the engine loads or the broker connects exits 0 (the
+    reference's main catches it around both, rpc_broker.py:107-119), and close()
+    survives a connection pika already closed."""
+    from inversekinematicsann_amd import rpc_broker as R
+
+    def interrupted(argv=None):
+        raise KeyboardInterrupt
+    monkeypatch.setattr(R, "get_ikine_engine_cli", interrupted)
+    assert R.main(["--method", "fabrik"]) == 0
+    assert "CTRL+C interrupted" in capsys.readouterr().out
+
+    class Dead:
+        def stop_consuming(self):
+            raise RuntimeError("connection already closed")
+
+        def close(self):
+            raise RuntimeError("connection already closed")
+    b = R.IkineRPCBroker.__new__(R.IkineRPCBroker)
+    b.channel = b.connection = Dead()
+    b.close()
