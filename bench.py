@@ -109,6 +109,9 @@ def parse():
     ap.add_argument("--end-to-end", type=int, default=1,
                     help="also time the host-pointer (PCIe-inclusive) path; 0 for profiling "
                          "runs, whose per-kernel averages it would mix in")
+    ap.add_argument("--cold", type=int, default=1,
+                    help="FABRIK: also time cold calls (work order forgotten); 0 for profiling "
+                         "runs, whose per-kernel averages they would mix in")
     ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r02", "pmc"),
                     help="committed PMC diagnosis summaries (pipe occupancy in the roofline)")
@@ -398,7 +401,8 @@ def run_fabrik(job, args, tol=None, max_iter=None):
         res["gather_chunks"] = job.sc.info()[2]
         res["gather_ms"] = st.gather_ms
     mx, sm, sum_iters, n_capped = _stats_over_ranks(job, st, res)
-    res["cold"] = cold_steps(ctx, step)
+    if args.cold:
+        res["cold"] = cold_steps(ctx, step)
     n = job.n_local
     res["mean_iters"] = sum_iters / job.total
     res["n_capped"] = int(n_capped)

@@ -77,14 +77,21 @@ __device__ __forceinline__ void stamp(unsigned long long *p) {
 #endif
 }
 
-// Activations with the hardware exp2 / reciprocal (1 ulp each); tanh has an
-// absolute error of ~1e-7.
+// Activations with the hardware exp2 / reciprocal (1 ulp each).  tanh is
+// 1 - 2 / (1 + e), e = exp2(2 log2(e) v): one exp, one add, one reciprocal and one
+// fma per element, absolute error <= ~2.5e-7 (tests/test_gpu_parity.py
+// ::test_ann_tanh_accuracy); the limits come out exactly (e = inf -> 1, e = 0 ->
+// -1) and NaN propagates.  The r02 form sign(v) (1 - e') / (1 + e'), e' =
+// exp2(-2 log2(e) |v|), needs a subtraction, a multiply and a sign copy more:
+// tools/ubench.hip `act` measured 39.0 -> 35.5 cycles per element slot (-9 %), and
+// exp2 from a degree-6 polynomial on the full-rate pipe (v_pk_fma_f32) instead of
+// v_exp_f32 58.5 (+50 %: v_exp_f32 issues in 8 cycles, the polynomial's range
+// reduction, six packed fmas and exponent insert in more) -- profiles/r03/ubench.
 template <int ACT>
 __device__ __forceinline__ float act_apply(float v) {
   if constexpr (ACT == IK_ACT_TANH) {
-    // sign(v) (1 - e) / (1 + e), e = exp(-2|v|); NaN propagates
-    const float e = __builtin_amdgcn_exp2f(-fabsf(2.885390081777927f * v));
-    return copysignf((1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e), v);
+    const float e = __builtin_amdgcn_exp2f(2.885390081777927f * v);
+    return __builtin_fmaf(-2.0f, __builtin_amdgcn_rcpf(1.0f + e), 1.0f);
   } else if constexpr (ACT == IK_ACT_RELU) {
     return fmaxf(v, 0.0f);
   } else if constexpr (ACT == IK_ACT_SIGMOID) {
@@ -94,25 +101,19 @@ __device__ __forceinline__ float act_apply(float v) {
   }
 }
 
-// Two elements at once: the adds / multiplies become packed-fp32 instructions
-// (v_pk_mul_f32 / v_pk_add_f32) and the two independent chains interleave, so
-// the epilogue issues ~5 instructions per element.
+// Two elements at once: the adds / multiplies / fmas become packed-fp32
+// instructions (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int ACT>
 __device__ __forceinline__ f32x2 act_apply2(f32x2 v) {
   if constexpr (ACT == IK_ACT_TANH) {
-    const f32x2 u = v * 2.885390081777927f;
-    f32x2 e;
-    e.x = __builtin_amdgcn_exp2f(-fabsf(u.x));
-    e.y = __builtin_amdgcn_exp2f(-fabsf(u.y));
-    const f32x2 n = 1.0f - e, d = 1.0f + e;
-    f32x2 r;
-    r.x = __builtin_amdgcn_rcpf(d.x);
-    r.y = __builtin_amdgcn_rcpf(d.y);
-    f32x2 t = n * r;
-    t.x = copysignf(t.x, v.x);
-    t.y = copysignf(t.y, v.y);
-    return t;
+    f32x2 e = v * 2.885390081777927f;
+    e.x = __builtin_amdgcn_exp2f(e.x);
+    e.y = __builtin_amdgcn_exp2f(e.y);
+    e = 1.0f + e;
+    e.x = __builtin_amdgcn_rcpf(e.x);
+    e.y = __builtin_amdgcn_rcpf(e.y);
+    return __builtin_elementwise_fma(e, f32x2{-2.0f, -2.0f}, f32x2{1.0f, 1.0f});
   } else {
     f32x2 t;
     t.x = act_apply<ACT>(v.x);
@@ -121,34 +122,29 @@ __device__ __forceinline__ f32x2 act_apply2(f32x2 v) {
   }
 }
 
-// Four pairs at once, phase by phase (see layer_store).
+// Four pairs at once, phase by phase (see layer_store): the dependent exp / rcp
+// chains of the eight elements overlap.
 template <int ACT>
 __device__ __forceinline__ void act_apply2x4(f32x2 (&v)[4]) {
   if constexpr (ACT == IK_ACT_TANH) {
-    f32x2 e[4], d[4];
+    f32x2 e[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) e[k] = v[k] * 2.885390081777927f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      e[k].x = __builtin_amdgcn_exp2f(-fabsf(e[k].x));
-      e[k].y = __builtin_amdgcn_exp2f(-fabsf(e[k].y));
+      e[k].x = __builtin_amdgcn_exp2f(e[k].x);
+      e[k].y = __builtin_amdgcn_exp2f(e[k].y);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) d[k] = 1.0f + e[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = 1.0f - e[k];
+    for (int k = 0; k < 4; ++k) e[k] = 1.0f + e[k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      d[k].x = __builtin_amdgcn_rcpf(d[k].x);
-      d[k].y = __builtin_amdgcn_rcpf(d[k].y);
+      e[k].x = __builtin_amdgcn_rcpf(e[k].x);
+      e[k].y = __builtin_amdgcn_rcpf(e[k].y);
     }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = e[k] * d[k];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      v[k].x = copysignf(e[k].x, v[k].x);
-      v[k].y = copysignf(e[k].y, v[k].y);
-    }
+    for (int k = 0; k < 4; ++k)
+      v[k] = __builtin_elementwise_fma(e[k], f32x2{-2.0f, -2.0f}, f32x2{1.0f, 1.0f});
   } else {
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = act_apply2<ACT>(v[k]);

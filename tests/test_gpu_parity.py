@@ -252,6 +252,37 @@ def test_ann_vs_oracle(ctx1, dims, act):
     assert d <= NS_TOL, d  # north_star: 1e-5 absolute
 
 
+@pytest.mark.parametrize("hidden", [True, False])
+def test_ann_tanh_accuracy(ctx1, hidden):
+    """The kernels' tanh (1 - 2 / (1 + exp2(2 log2(e) v)), hardware exp2 and
+    reciprocal) against float64 tanh: absolute error <= 3e-7 (2.5 fp32 ulps at
+    |tanh| in [0.5, 1)) over [-12, 12], exact +-1 in saturation, for the hidden-layer
+    epilogue (3 -> 32 tanh -> 4 linear, identity weights) and the 4-wide output layer
+    (3 -> 4 tanh).  Scalers are the identity, so the outputs are tanh(f32(p))."""
+    rng = np.random.default_rng(3)
+    n = 20_000
+    pts = np.concatenate([rng.uniform(-12, 12, (n, 3)), rng.uniform(-1e-3, 1e-3, (2000, 3)),
+                          np.array([[0.0, -0.0, 30.0], [1e30, -1e30, 9.1], [-9.1, 1e-30, 1.0]])])
+    if hidden:
+        W1 = np.zeros((3, 32), np.float32)
+        W1[0, 0] = W1[1, 1] = W1[2, 2] = 1.0
+        W2 = np.zeros((32, 4), np.float32)
+        W2[0, 0] = W2[1, 1] = W2[2, 2] = 1.0
+        Ws, bs, acts = [W1, W2], [np.zeros(32, np.float32), np.zeros(4, np.float32)], \
+            ["tanh", "linear"]
+    else:
+        W = np.zeros((3, 4), np.float32)
+        W[0, 0] = W[1, 1] = W[2, 2] = 1.0
+        Ws, bs, acts = [W], [np.zeros(4, np.float32)], ["tanh"]
+    ctx1.ann_load(Ws, bs, acts, np.zeros(3), np.ones(3), np.zeros(4), np.ones(4))
+    ang, _, _ = ctx1.ann_solve(pts, check_limits=False)
+    ref = np.tanh(pts.astype(np.float32).astype(np.float64))
+    err = np.abs(ang[:, :3].astype(np.float64) - ref)
+    assert err.max() <= 3e-7, float(err.max())
+    big = np.abs(pts) >= 9.1
+    assert np.array_equal(ang[:, :3][big], np.sign(pts[big]).astype(np.float32))
+
+
 def test_ann_width_cap(ctx1):
     """ik_ann_load takes widths up to 1024 and refuses only wider layers."""
     from inversekinematicsann_amd import _native
