@@ -112,8 +112,9 @@ def parse():
     ap.add_argument("--cold", type=int, default=1,
                     help="FABRIK: also time cold calls (work order forgotten); 0 for profiling "
                          "runs, whose per-kernel averages they would mix in")
-    ap.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r02", "pmc"),
+    ap.add_argument("--traffic-file",
+                    default=os.path.join(ROOT, "profiles", "r03", "traffic.json"))
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r03", "pmc"),
                     help="committed PMC diagnosis summaries (pipe occupancy in the roofline)")
     ap.add_argument("--gather", type=int, default=1,
                     help="N>1: the sharded solve with the library's RCCL all-gather of every "
@@ -189,15 +190,31 @@ def _batch_words(job) -> str:
     return f"{_pts(job.total)} random_dist points over {job.world} GPUs ({how})"
 
 
-def load_traffic(path, kernel):
-    """HBM bytes per launch of `kernel` from the PMC pass (tools/pmc_traffic.py),
-    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM; None if not collected."""
+def load_profile(path, kernel):
+    """What the profiling lease (tools/profile_round.sh -> tools/profile_summary.py)
+    recorded for `kernel` over the bench's timed window, or {}."""
     try:
         with open(path) as f:
-            d = json.load(f)
-        return d.get(kernel, {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(kernel, {}) or {}
     except (OSError, ValueError):
-        return None
+        return {}
+
+
+def load_traffic(path, kernel):
+    """HBM bytes per launch of `kernel` from the PMC passes, FETCH_SIZE doubled per
+    MI355X_MICROARCH.md §HBM; None if not collected."""
+    return load_profile(path, kernel).get("hbm_bytes_per_launch")
+
+
+def profile_fields(path, kernel):
+    """The roofline's profile-derived extras: the raw (undoubled) HBM bytes, the
+    kernel's shader clock and the rocprof window average of its duration."""
+    p = load_profile(path, kernel)
+    out = {k: p[k] for k in ("hbm_bytes_per_launch_raw", "clock_ghz", "rocprof_avg_ms")
+           if k in p}
+    if out:
+        out["profile"] = os.path.relpath(path, ROOT)
+    return out
 
 
 def load_pipe(path, kernel):
@@ -210,11 +227,14 @@ def load_pipe(path, kernel):
     except (OSError, ValueError):
         return None
     for k, v in d.items():
-        if k.split("<")[0] == kernel:
-            return {"mfma_busy": v.get("MfmaUtil_pct", 0.0) / 100,
-                    "valu_active": v.get("ValuActive_pct", 0.0) / 100,
-                    "fp64_pipe_busy": v.get("Fp64PipeBusy_pct", 0.0) / 100,
-                    "source": os.path.relpath(path, ROOT)}
+        if k == kernel or k.split("<")[0] == kernel:
+            out = {"mfma_busy": v.get("MfmaUtil_pct", 0.0) / 100,
+                   "valu_active": v.get("ValuActive_pct", 0.0) / 100,
+                   "fp64_pipe_busy": v.get("Fp64PipeBusy_pct", 0.0) / 100,
+                   "source": os.path.relpath(path, ROOT)}
+            if "L2_hit_pct" in v:
+                out["l2_hit"] = v["L2_hit_pct"] / 100
+            return out
     return None
 
 
@@ -357,9 +377,9 @@ def run_ann(job, args, mode="fp32"):
                        "frac": achieved / peak if achieved else None,
                        "traffic": traffic, "kernel": kname,
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
-                       "points_per_launch": n}
+                       "points_per_launch": n, **profile_fields(args.traffic_file, kname)}
     diag = "ann_diag_summary.json" if mode == "fp32" else f"ann_{mode}_diag_summary.json"
-    res["roofline"]["pipes"] = load_pipe(os.path.join(args.pmc_dir, diag), "ann_fused_kernel")
+    res["roofline"]["pipes"] = load_pipe(os.path.join(args.pmc_dir, diag), kname)
     if mode == "fp32":
         res["dtype"] = "fp32"
         res["workload"] = ("ANN MLP forward (3-12x500tanh-4, fp32) + fused FK round-trip error, "
@@ -418,18 +438,22 @@ def run_fabrik(job, args, tol=None, max_iter=None):
     k = res["kernels"].get("fabrik_iter_kernel")
     flops = FABRIK_FLOP_PER_ITER * local_iters
     achieved = flops / (k / 1e3) if k else None
-    traffic = load_traffic(args.traffic_file, "fabrik_iter_kernel")
+    pkey = "fabrik_iter_kernel" if (tol, max_iter) != (1e-5, 200) else \
+        "fabrik_tol1e-5/fabrik_iter_kernel"
+    traffic = load_traffic(args.traffic_file, pkey)
     res["roofline"] = {"bound": "valu_fp64", "achieved": achieved / 1e12 if achieved else None,
                        "peak": FP64_VALU_PEAK / 1e12, "unit": "TFLOP/s",
                        "frac": achieved / FP64_VALU_PEAK if achieved else None,
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
                        "iterations_per_launch": local_iters,
+                       **profile_fields(args.traffic_file, pkey),
                        # the flop count prices a correctly rounded sqrt / division as
                        # one flop; the pipes say how busy the SIMDs actually are
-                       "pipes": load_pipe(os.path.join(args.pmc_dir,
-                                                       "fabrik_diag_summary.json"),
-                                          "fabrik_iter_kernel")}
+                       "pipes": load_pipe(os.path.join(
+                           args.pmc_dir, "fabrik_diag_summary.json" if pkey ==
+                           "fabrik_iter_kernel" else "fabrik_tol1e-5_diag_summary.json"),
+                           "fabrik_iter_kernel")}
     res["dtype"] = "f64"
     res["workload"] = (f"FABRIK ikine (seed FK + loop + angles) + fused FK round-trip error, "
                        f"tol {tol:g} / {max_iter} iterations, float64, " + _batch_words(job))
@@ -464,6 +488,7 @@ def run_fk(job, args):
                        "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                        "frac": achieved / HBM_PEAK if achieved else None,
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
+                       **profile_fields(args.traffic_file, "fk_kernel"),
                        "kernel": "fk_kernel", "kernel_ms": k,
                        "algorithmic_bytes_per_point": FK_BYTES_PER_POINT,
                        "points_per_launch": n}

@@ -255,7 +255,7 @@ int ik_comm_destroy(ik_ctx *ctx);
  * before one), so a caller can find its own rows with ik_shard_part. */
 int ik_comm_info(ik_ctx *ctx, int *nranks, int *rank, int *last_chunks);
 /* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic: FABRIK
- * 4 when a rank's share is >= 256k rows, else 1; ANN 1 (its gather is ~1 % of
+ * 2 when a rank's share is >= 512k rows, else 1; ANN 1 (its gather is ~1 % of
  * its solve).  Environment default: IKHIP_GATHER_CHUNKS. */
 int ik_comm_set_chunks(ik_ctx *ctx, int chunks);
 /* Host-only helpers of the protocol (no device needed). */

@@ -235,8 +235,11 @@ int auto_chunks(ik_ctx *c, int method, int64_t n) {
     }
     C = env;
   }
-  if (C <= 0)  // automatic: overlap only where the gather is comparable to the solve
-    C = (method == IK_METHOD_FABRIK && m.nranks > 1 && n / m.nranks >= 262144) ? 4 : 1;
+  // automatic: overlap only where the gather is comparable to the solve, and in
+  // two chunks: every FABRIK launch has a tail of its own (its last long points),
+  // so four 250k-point launches cost ~1.6x one 1M-point launch (0.15 ms each
+  // against 0.38 ms, profiles/r03/e2e) while two 500k-point ones cost ~1.15x
+  if (C <= 0) C = (method == IK_METHOD_FABRIK && m.nranks > 1 && n / m.nranks >= 524288) ? 2 : 1;
   return C > IK_MAX_GATHER_CHUNKS ? IK_MAX_GATHER_CHUNKS : C;
 }
 

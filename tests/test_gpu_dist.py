@@ -116,7 +116,7 @@ def test_sharded_solves_over_library_rccl():
 
 def _fullsize_worker(q):
     """configs[3] / configs[4]'s whole 10M-point seed-1 batch through the sharded
-    solves at one rank (FABRIK in 4 chunks, the automatic count at 8 ranks), against
+    solves at one rank (FABRIK in 4 chunks, set explicitly: one rank plans 1), against
     the plain solve, bit for bit."""
     import torch
     from inversekinematicsann_amd import _native
