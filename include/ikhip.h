@@ -249,6 +249,13 @@ int ik_comm_unique_id(uint8_t *id /* IK_COMM_ID_BYTES */);
 /* Collective over the nranks processes: binds the context to an RCCL
  * communicator (one GPU per rank). */
 int ik_comm_init(ik_ctx *ctx, int nranks, int rank, const uint8_t *id);
+/* TEST-ONLY: a communicator without RCCL, so that one GPU can run the sharded
+ * path as rank `rank` of `nranks` (the placement of every part, the ragged
+ * chunk's stage, the tail reduction).  Its all-gather writes byte o of rank
+ * s's slot as ik_loopback_byte(s, o) for every s != rank, and copies this
+ * rank's tail block into every rank's. */
+int ik_comm_init_loopback(ik_ctx *ctx, int nranks, int rank);
+int ik_loopback_byte(int slot, int64_t offset);
 int ik_comm_destroy(ik_ctx *ctx);
 /* The communicator as the library holds it: ranks, this rank, and the chunk
  * count the last sharded call was planned with (ik_shard_plan_of's chunks; 0

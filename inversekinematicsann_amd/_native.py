@@ -35,7 +35,8 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_fabrik_reset_order", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode",
-                    "ik_comm_unique_id", "ik_comm_init", "ik_comm_destroy", "ik_comm_info",
+                    "ik_comm_unique_id", "ik_comm_init", "ik_comm_init_loopback",
+                    "ik_loopback_byte", "ik_comm_destroy", "ik_comm_info",
                     "ik_comm_set_chunks", "ik_shard_plan_of", "ik_shard_part", "ik_shard_range",
                     "ik_tail_reduce", "ik_fkhist_bin", "ik_fkhist_upper", "ik_fk_err_quantile",
                     "ik_ann_solve_sharded", "ik_fabrik_solve_sharded", "ik_host_alloc",
@@ -135,6 +136,8 @@ def load_library(path: str = LIB_PATH):
         L.ik_host_free.argtypes = [vp]
         L.ik_comm_unique_id.argtypes = [vp]
         L.ik_comm_init.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        L.ik_comm_init_loopback.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.ik_loopback_byte.argtypes = [ctypes.c_int, i64]
         L.ik_comm_destroy.argtypes = [vp]
         ipt = ctypes.POINTER(ctypes.c_int)
         L.ik_comm_info.argtypes = [vp, ipt, ipt, ipt]
@@ -431,6 +434,11 @@ class Context:
             raise ValueError(f"unique id must be {IK_COMM_ID_BYTES} bytes")
         buf = ctypes.create_string_buffer(bytes(uid), IK_COMM_ID_BYTES)
         self._check(self.lib.ik_comm_init(self.handle, int(nranks), int(rank), buf))
+
+    def comm_init_loopback(self, nranks: int, rank: int):
+        """TEST-ONLY (ik_comm_init_loopback): rank `rank` of `nranks` on this one GPU,
+        no RCCL; the other ranks' gathered rows come back as loopback_byte patterns."""
+        self._check(self.lib.ik_comm_init_loopback(self.handle, int(nranks), int(rank)))
 
     def comm_destroy(self):
         self._check(self.lib.ik_comm_destroy(self.handle))

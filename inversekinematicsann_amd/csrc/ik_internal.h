@@ -32,7 +32,8 @@ struct IkTailBlock {
 // chunked in-place all-gathers of the sharded solves (ik_shard.hip), grow-only
 // like the scratch.
 struct IkComm {
-  void *comm = nullptr;  // ncclComm_t
+  void *comm = nullptr;  // ncclComm_t (a non-null sentinel for a loopback communicator)
+  bool loopback = false;  // ik_comm_init_loopback (test-only): no RCCL, see ik_shard.hip
   int nranks = 0, rank = -1;
   int chunks_req = 0;    // ik_comm_set_chunks (0 = automatic)
   int last_chunks = 0;   // all-gathers of the last sharded call (its plan's chunks)

@@ -220,6 +220,27 @@ __global__ void pack_tail_kernel(TailArgs a, ik_shard_tail *t) {
   *t = o;
 }
 
+// ik_comm_init_loopback's all-gather (test-only): one GPU plays rank `me` of g.
+// The other ranks' slots of the receive buffer get a fixed byte pattern of
+// (slot, byte offset), ik_loopback_byte, so a test can check where the plan put
+// every foreign row (in place and through the stage); tail blocks (replicate)
+// get a copy of this rank's.
+__host__ __device__ inline uint8_t loopback_byte(int slot, uint64_t o) {
+  return (uint8_t)(((uint32_t)slot * 29u + (uint32_t)o * 13u + (uint32_t)(o >> 7)) ^ 0xA5u);
+}
+
+__global__ __launch_bounds__(256) void loopback_gather_kernel(const uint8_t *send, uint8_t *recv,
+                                                              uint64_t cnt, int g, int me,
+                                                              int replicate) {
+  const uint64_t tot = cnt * (uint64_t)g;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const int s = (int)(i / cnt);
+    const uint64_t o = i - (uint64_t)s * cnt;
+    recv[i] = (s == me || replicate) ? send[o] : loopback_byte(s, o);  // in place: same byte
+  }
+}
+
 }  // namespace ikhip
 
 namespace {
@@ -308,9 +329,28 @@ int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nr
                 double *fk_err_dev, Solve solve) {
   IkComm &m = c->comm;
   Rccl *r = nullptr;
-  int rc = load_rccl(&r);
+  int rc = m.loopback ? IK_OK : load_rccl(&r);
   if (rc) return rc;
   const int g = m.nranks, me = m.rank, C = P.chunks;
+  // one all-gather of cnt bytes per rank on the comm stream (inside a group)
+  auto gather = [&](const void *send, void *recv, size_t cnt, bool replicate) -> int {
+    if (m.loopback) {
+      const uint64_t tot = (uint64_t)cnt * g, blocks = (tot + 255) / 256;
+      if (tot)
+        hipLaunchKernelGGL(loopback_gather_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)),
+                           dim3(256), 0, m.cs, static_cast<const uint8_t *>(send),
+                           static_cast<uint8_t *>(recv), (uint64_t)cnt, g, me, replicate ? 1 : 0);
+      IK_HIP(hipGetLastError());
+      return IK_OK;
+    }
+    const int res = r->all_gather(send, recv, cnt, kNcclUint8, m.comm, m.cs);
+    return res ? rccl_fail(r, "ncclAllGather", res) : IK_OK;
+  };
+  auto group = [&](bool start) -> int {
+    if (m.loopback) return IK_OK;
+    const int res = start ? r->group_start() : r->group_end();
+    return res ? rccl_fail(r, start ? "ncclGroupStart" : "ncclGroupEnd", res) : IK_OK;
+  };
   const int64_t S = P.part_rows;
   m.last_chunks = C;
   m.last_hist = fk_err_dev != nullptr;
@@ -358,26 +398,18 @@ int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nr
     // chunk k's rows of every rank, in place (+ every rank's tail block with the last)
     kt_begin("rccl_all_gather", m.cs);
     IK_HIP(hipEventRecord(m.ev_gs[k], m.cs));
-    int res = r->group_start();
-    if (res != 0) return rccl_fail(r, "ncclGroupStart", res);
-    for (int q = 0; q < nreg; ++q) {
+    if ((rc = group(true))) return rc;
+    for (int q = 0; q < nreg && !rc; ++q) {
       char *base = staged ? R[q].stage : R[q].out + cb * R[q].rb;
       const size_t cnt = (size_t)S * R[q].rb;
-      res = r->all_gather(base + (size_t)me * cnt, base, cnt, kNcclUint8, m.comm, m.cs);
-      if (res != 0) {
-        (void)r->group_end();
-        return rccl_fail(r, "ncclAllGather", res);
-      }
+      rc = gather(base + (size_t)me * cnt, base, cnt, false);
     }
-    if (last) {
-      res = r->all_gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), kNcclUint8, m.comm, m.cs);
-      if (res != 0) {
-        (void)r->group_end();
-        return rccl_fail(r, "ncclAllGather", res);
-      }
+    if (last && !rc) rc = gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), true);
+    if (rc) {
+      (void)group(false);
+      return rc;
     }
-    res = r->group_end();
-    if (res != 0) return rccl_fail(r, "ncclGroupEnd", res);
+    if ((rc = group(false))) return rc;
     IK_HIP(hipEventRecord(m.ev_ge[k], m.cs));
     kt_end(m.cs);
     if (staged && cb < P.n)  // the ragged chunk: its rows are in global order in the stage
@@ -393,9 +425,7 @@ int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nr
     IK_HIP(hipEventRecord(m.ev_solved[0], c->stream));
     IK_HIP(hipStreamWaitEvent(m.cs, m.ev_solved[0], 0));
     IK_HIP(hipEventRecord(m.ev_gs[0], m.cs));
-    const int res =
-        r->all_gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), kNcclUint8, m.comm, m.cs);
-    if (res != 0) return rccl_fail(r, "ncclAllGather", res);
+    if ((rc = gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), true))) return rc;
     IK_HIP(hipEventRecord(m.ev_ge[0], m.cs));
     m.last_chunks = 1;
   }
@@ -435,7 +465,7 @@ int sharded_stats(ik_ctx *c, ik_stats *stats) {
 void comm_release(ik_ctx *c) {
   IkComm &m = c->comm;
   if (m.cs) (void)hipStreamSynchronize(m.cs);
-  if (m.comm) {
+  if (m.comm && !m.loopback) {
     Rccl *r = nullptr;
     if (load_rccl(&r) == IK_OK) (void)r->comm_destroy(m.comm);
   }
@@ -492,6 +522,22 @@ int ik_comm_init(ik_ctx *c, int nranks, int rank, const uint8_t *id) {
   c->comm.rank = rank;
   return IK_OK;
 }
+
+int ik_comm_init_loopback(ik_ctx *c, int nranks, int rank) {
+  if (!c || nranks < 1 || nranks > 1024 || rank < 0 || rank >= nranks)
+    return fail(IK_E_BADARG, "ik_comm_init_loopback: bad args");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  (void)hipStreamSynchronize(c->stream);
+  comm_release(c);
+  c->comm.comm = &c->comm;  // a sentinel: never passed to RCCL
+  c->comm.loopback = true;
+  c->comm.nranks = nranks;
+  c->comm.rank = rank;
+  return IK_OK;
+}
+
+int ik_loopback_byte(int slot, int64_t offset) { return loopback_byte(slot, (uint64_t)offset); }
 
 int ik_comm_destroy(ik_ctx *c) {
   if (!c) return fail(IK_E_BADARG, "ik_comm_destroy: NULL context");

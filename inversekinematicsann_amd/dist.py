@@ -82,6 +82,15 @@ class ShardedContext:
         self.rank = int(rank)
         ctx.comm_init(self.world, self.rank, uid)
 
+    @classmethod
+    def loopback(cls, ctx: _native.Context, world: int, rank: int) -> "ShardedContext":
+        """TEST-ONLY: rank `rank` of `world` on one GPU without RCCL
+        (ik_comm_init_loopback); see loopback_bytes for the other ranks' rows."""
+        self = cls.__new__(cls)
+        self.ctx, self.world, self.rank = ctx, int(world), int(rank)
+        ctx.comm_init_loopback(self.world, self.rank)
+        return self
+
     def close(self):
         self.ctx.comm_destroy()
 
@@ -123,6 +132,34 @@ def init_from_env(ctx: _native.Context) -> ShardedContext:
 
 
 # ---- host mirror of the protocol ---------------------------------------------
+def loopback_bytes(slot: int, offsets: np.ndarray) -> np.ndarray:
+    """ik_loopback_byte for many offsets: the bytes a loopback communicator's
+    all-gather writes into rank `slot`'s part (numpy restatement)."""
+    o = np.asarray(offsets, np.uint64)
+    v = (np.uint64(slot * 29) + o * np.uint64(13) + (o >> np.uint64(7))) & np.uint64(0xFFFFFFFF)
+    return ((v ^ np.uint64(0xA5)) & np.uint64(0xFF)).astype(np.uint8)
+
+
+def loopback_expected(n: int, world: int, rank: int, chunks: int, row_bytes: int,
+                      own: np.ndarray) -> np.ndarray:
+    """The whole gathered array (n rows of row_bytes) as rank `rank` of a loopback
+    communicator holds it after a sharded call: its own parts from `own` (the
+    full-batch rows a plain solve gives), every other rank's part filled with
+    loopback_bytes of (that rank, byte offset within its part)."""
+    own = np.ascontiguousarray(own).view(np.uint8).reshape(n, row_bytes)
+    out = np.empty((n, row_bytes), np.uint8)
+    C, _, _ = plan_of(n, world, chunks)
+    for c in range(C):
+        for r in range(world):
+            b, e = part_bounds(n, world, chunks, r, c)
+            if e <= b:
+                continue
+            if r == rank:
+                out[b:e] = own[b:e]
+            else:
+                out[b:e] = loopback_bytes(r, np.arange((e - b) * row_bytes)).reshape(-1, row_bytes)
+    return out
+
 def fkhist(err: np.ndarray) -> np.ndarray:
     """A rank's FK-error histogram (IK_FKHIST_BINS uint32), numpy restatement of
     fkhist_bin: 16 bins per octave from the float64 exponent and top 4 mantissa

@@ -7,7 +7,9 @@ host outputs, and at configs[3] / configs[4]'s full 10M-point seed-1 batch.  No
 torch.distributed: the C-ABI caller's view.  The N > 1
 bookkeeping (the chunk plan, in-place placement, tail reduction, lowest global
 failing index, histograms) is covered by the gloo tests in test_dist_gloo.py;
-the 8-GPU run is the driver's scaling bench."""
+the 8-GPU run is the driver's scaling bench.  The device side of g > 1 (part
+placement, the ragged chunk's stage, the tail reduction) runs on one GPU through
+the test-only loopback communicator (ik_comm_init_loopback)."""
 import numpy as np
 import pytest
 
@@ -172,3 +174,113 @@ def test_sharded_full_size_10m_equals_plain_solve():
         assert abs(s1["sum_fk_err"] - s2["sum_fk_err"]) <= 1e-9 * max(1.0, s1["sum_fk_err"])
         assert s2["gather_ms"] > 0
     assert res["fabrik"][5][2] == 4 and res["ann"][5][2] == 1
+
+
+def _loopback_worker(q):
+    """One GPU as rank r of g = 2, 3 (ik_comm_init_loopback: no RCCL): the device
+    code of the N > 1 path -- every part placed at its plan rows, the ragged
+    chunk's stage copied out truncated at n, empty parts (n < g), the tails
+    reduced -- against a single-context solve and the loopback byte pattern."""
+    import torch
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd import dist as D
+    from inversekinematicsann_amd.kinematics.ann import (REFERENCE_X_SCALER as XS,
+                                                         REFERENCE_Y_SCALER as YS, glorot_model)
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    try:
+        ctx = _native.Context(0)
+        pts = random_dist(5000, seed=5)
+        pts[3400] = [1.0, 2.0, -3.5]  # out of reach, in rank 1's or 2's rows
+        pts[4990] = [0.0, 0.0, 2.0]   # ZeroDivisionError, in the ragged chunk
+        m = glorot_model(dims=(3, 64, 64, 4), seed=4)
+        ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+        out = []
+        for n, cases in ((5000, ((2, 1), (2, 3), (3, 3), (3, 8))), (2, ((3, 1),)),
+                         (0, ((2, 1),))):
+            p = pts[:n]
+            f_ang, f_it, f_err, f_st = ctx.fabrik_solve_fk(p, 1e-3, 100)
+            a_ang, a_err, a_st = ctx.ann_solve(p, want_fk_err=True)
+            dpts = torch.from_numpy(p).cuda()
+            for g, chunks in cases:
+                per_rank = []
+                for r in range(g):
+                    sc = D.ShardedContext.loopback(ctx, g, r)
+                    sc.set_chunks(chunks)
+                    own = np.zeros(n, bool)
+                    C, _, _ = D.plan_of(n, g, chunks)
+                    for c in range(C):
+                        b, e = D.part_bounds(n, g, chunks, r, c)
+                        own[b:e] = True
+                    ang, it, err, st = sc.fabrik(p, 1e-3, 100, want_fk_err=True)
+                    ok = {
+                        "fab_ang": np.array_equal(ang.view(np.uint8).reshape(n, 32), D.loopback_expected(
+                            n, g, r, chunks, 32, f_ang)),
+                        "fab_it": np.array_equal(it.view(np.uint8).reshape(n, 4), D.loopback_expected(
+                            n, g, r, chunks, 4, f_it)),
+                        "fab_err_own": np.array_equal(err[own], f_err[own], equal_nan=True),
+                        "info": sc.info() == (g, r, chunks)}
+                    if n and own.any():
+                        ok["p99"] = sc.fk_err_quantile(0.99) == D.hist_quantile(
+                            [D.fkhist(f_err[own])], 0.99)
+                    fst = st.as_dict()
+                    dang = torch.full((n, 4), 7.0, dtype=torch.float64, device="cuda")
+                    dit = torch.full((n,), -9, dtype=torch.int32, device="cuda")
+                    derr = torch.full((n,), -1.0, dtype=torch.float64, device="cuda")
+                    dst = sc.fabrik_device(dpts, dang, dit, derr, 1e-3, 100).as_dict()
+                    ok["fab_dev_ang"] = np.array_equal(
+                        dang.cpu().numpy().view(np.uint8).reshape(n, 32),
+                        D.loopback_expected(n, g, r, chunks, 32, f_ang))
+                    ok["fab_dev_it"] = np.array_equal(
+                        dit.cpu().numpy().view(np.uint8).reshape(n, 4),
+                        D.loopback_expected(n, g, r, chunks, 4, f_it))
+                    e_dev = derr.cpu().numpy()
+                    ok["fab_dev_err"] = (np.array_equal(e_dev[own], f_err[own], equal_nan=True)
+                                         and bool((e_dev[~own] == -1.0).all()))
+                    # (the FK-error sum is a float reduction in no fixed order)
+                    exact = [k for k in fst if k not in ("gather_ms", "sum_fk_err")]
+                    ok["fab_dev_stats"] = ({k: dst[k] for k in exact} == {k: fst[k] for k in exact}
+                                           and abs(dst["sum_fk_err"] - fst["sum_fk_err"])
+                                           <= 1e-9 * max(1.0, fst["sum_fk_err"]))
+                    aang, aerr, ast = sc.ann(p, want_fk_err=True)
+                    ok["ann_ang"] = np.array_equal(aang.view(np.uint8).reshape(n, 16),
+                                                   D.loopback_expected(n, g, r, chunks, 16, a_ang))
+                    ok["ann_err_own"] = np.array_equal(aerr[own], a_err[own], equal_nan=True)
+                    fang = torch.zeros((n, 4), dtype=torch.float32, device="cuda")
+                    sc.ann_device(dpts, fang, derr)
+                    ok["ann_dev_ang"] = np.array_equal(
+                        fang.cpu().numpy().view(np.uint8).reshape(n, 16),
+                        D.loopback_expected(n, g, r, chunks, 16, a_ang))
+                    per_rank.append((ok, fst, ast.as_dict()))
+                    sc.close()
+                out.append(((n, g, chunks), per_rank, f_st.as_dict(), a_st.as_dict()))
+        q.put(out)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put(repr(e) + traceback.format_exc())
+
+
+def test_sharded_placement_at_2_and_3_ranks_loopback():
+    """the sharded path's device code at g > 1 on one GPU.  Per rank:
+    the whole gathered array equals its own rows of a plain solve plus the
+    loopback pattern in every other rank's rows (host and device outputs, FABRIK
+    32 + 4 B rows, ANN 16 B), FK errors written for its own rows only, the quantile
+    from its own histogram; over the g ranks (each tail copied g times by the
+    loopback), the stats add up to the plain solve's: lowest global failing
+    indices, iteration sums, FK-error max and sum."""
+    res = _spawn(_loopback_worker, timeout=300)
+    for (n, g, chunks), per_rank, f_st, a_st in res:
+        for r, (ok, fst, ast) in enumerate(per_rank):
+            bad = [k for k, v in ok.items() if not v]
+            assert not bad, ((n, g, chunks, r), bad)
+        for st, ref in (([x[1] for x in per_rank], f_st), ([x[2] for x in per_rank], a_st)):
+            for k in ("first_oob", "first_err"):
+                got = [s[k] for s in st if s[k] >= 0]
+                assert (min(got) if got else -1) == ref[k], ((n, g, chunks), k)
+            for k in ("sum_iters", "n_capped"):
+                assert sum(s[k] for s in st) == g * ref[k], ((n, g, chunks), k)
+            assert max(s["max_iters"] for s in st) == ref["max_iters"]
+            assert max(s["max_fk_err"] for s in st) == ref["max_fk_err"]
+            tot = sum(s["sum_fk_err"] for s in st) / g
+            assert abs(tot - ref["sum_fk_err"]) <= 1e-9 * max(1.0, ref["sum_fk_err"])
+        if n == 5000:
+            assert f_st["first_oob"] == 3400 and f_st["first_err"] == 4990
