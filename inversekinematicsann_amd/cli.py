@@ -13,8 +13,10 @@ a ZeroDivisionError propagates.  Plotting (plot/plot.py) is out of scope:
 --verbose prints the angles and the FK round-trip error instead of plotting.
 Extra flags: --tol / --max-iter (FABRIK, defaults 1e-3 / 100 as the
 reference's constructor) and --device.
-`--generate-data` supports the two shapes the benchmarks use (spring,
-random_dist normal); the other generators are out of scope.
+`--generate-data --shape {circle,cube,cube_random,random,spring,random_dist}` runs
+the reference's generators (robot/position_generator.py, cli.py:80-229) with the
+same arguments: --to-file writes the x,y,z CSV, --verbose prints the shape's
+parameters as the reference does (its 3-D plot is out of scope).
 """
 from __future__ import annotations
 
@@ -27,10 +29,19 @@ import numpy as np
 EXAMPLES = {
     "ann": "--inverse-kine --method ann --model model_filename.h5 --points filename.csv",
     "fabrik": "--inverse-kine --method fabrik --points filename.csv",
+    "circle": "--generate-data --shape circle --radius 3 --samples 20 --center 1,5,2",
+    "cube": "--generate-data --shape cube --step 0.75 --dim 2,3,4 --start 1,2,3",
+    "cube_random": "--generate-data --shape cube_random --step 0.75 --dim 2,3,4 --start 1,2,3",
+    "random": "--generate-data --shape random --limits 0,3;0,4;0,5 --samples 20",
     "spring": "--generate-data --shape spring --samples 50 --dim 2,3,6",
     "random_dist": "--generate-data --shape random_dist --dist normal --samples 100 "
                    "--std_dev 0.35 --limits 0,3;0,4;0,5",
 }
+# each shape's required arguments (cli.py:91-94, 117-119, 155-157, 182-184, 206-211)
+SHAPE_ARGS = {"circle": ("radius", "samples", "center"), "cube": ("step", "dim", "start"),
+              "cube_random": ("step", "dim", "start"), "random": ("samples", "limits"),
+              "spring": ("samples", "dim"),
+              "random_dist": ("dist", "samples", "std_dev", "limits")}
 
 
 def _parser():
@@ -39,7 +50,7 @@ def _parser():
     g.add_argument("--inverse-kine", action="store_true")
     g.add_argument("--generate-data", action="store_true")
     p.add_argument("--method", choices=["ann", "fabrik"])
-    p.add_argument("--shape", choices=["spring", "random_dist"])
+    p.add_argument("--shape", choices=list(SHAPE_ARGS))
     p.add_argument("--example", action="store_true")
     p.add_argument("--points", type=str, help=".csv file name with stored trajectory points")
     p.add_argument("--model", type=str, help="select saved model .h5 (or .npz) filename")
@@ -53,9 +64,13 @@ def _parser():
     # data generators
     p.add_argument("--samples", type=int)
     p.add_argument("--dim", type=str)
-    p.add_argument("--dist", type=str, choices=["normal"])
+    p.add_argument("--dist", type=str, choices=["normal", "uniform", "random"])
     p.add_argument("--std_dev", type=float)
     p.add_argument("--limits", type=str)
+    p.add_argument("--radius", type=float)
+    p.add_argument("--center", type=str)
+    p.add_argument("--step", type=float)
+    p.add_argument("--start", type=str)
     return p
 
 
@@ -114,27 +129,53 @@ def _ikine(args, parser):
     return 0
 
 
+def _floats(text):
+    return [float(v) for v in text.split(",")]
+
+
+def _limits(text):
+    lim = text.split(";")
+    return {"x": _floats(lim[0]), "y": _floats(lim[1]), "z": _floats(lim[2])}
+
+
 def _generate(args, parser):
+    """cli.py:80-229: the shape's generator on its arguments; --verbose prints the
+    arguments tuple (the reference's ShapeCommand.verbose, before its plot),
+    --to-file the points as an x,y,z CSV."""
     import pandas as pd
-    from .robot.position_generator import random_dist, spring
+    from .robot import position_generator as G
     if args.shape is None:
         parser.error("the following arguments are required: --shape")
     if args.example:
         print(EXAMPLES[args.shape])
         return 0
-    if args.shape == "spring":
-        if args.samples is None or args.dim is None:
-            parser.error("the following arguments are required: --samples, --dim")
-        pts = spring(args.samples, *[float(v) for v in args.dim.split(",")])
+    missing = [a for a in SHAPE_ARGS[args.shape] if getattr(args, a) is None]
+    if missing:
+        parser.error("the following arguments are required: " +
+                     ", ".join("--" + a for a in missing))
+    sh = args.shape
+    if sh == "circle":
+        center = _floats(args.center)
+        params = (args.radius, args.samples, center)
+        pts = G.circle(args.radius, args.samples, center)
+    elif sh in ("cube", "cube_random"):
+        dim, start = _floats(args.dim), _floats(args.start)
+        params = (args.step, dim, start)
+        pts = (G.cube if sh == "cube" else G.cube_random)(args.step, *dim, start)
+    elif sh == "random":
+        lim = _limits(args.limits)
+        params = (args.samples, lim)
+        pts = G.random(args.samples, lim)
+    elif sh == "spring":
+        dim = _floats(args.dim)
+        params = (args.samples, *dim)
+        pts = G.spring(args.samples, *dim)
     else:
-        if None in (args.samples, args.std_dev, args.limits, args.dist):
-            parser.error("the following arguments are required: --dist, --samples, --std_dev, "
-                         "--limits")
-        lim = [[float(v) for v in ax.split(",")] for ax in args.limits.split(";")]
-        pts = random_dist(args.samples, seed=0, std_dev=args.std_dev,
-                          limits={"x": lim[0], "y": lim[1], "z": lim[2]})
+        lim = _limits(args.limits)
+        params = (args.samples, lim, args.dist, args.std_dev)
+        pts = G.random_distribution(args.samples, lim, args.dist, args.std_dev)
     if args.verbose:
-        print(pts.tolist())
+        print(params)
     if args.to_file is not None:
         pd.DataFrame(pts.tolist(), columns=["x", "y", "z"]).to_csv(args.to_file, index=False)
     return 0
