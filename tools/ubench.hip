@@ -11,6 +11,8 @@
 //               full-rate pipe (the VERDICT r02 proposal) instead of v_exp_f32.
 //  lat   K      dependent-chain latency of one instruction kind (K 0 v_fma_f64,
 //               1 v_rcp_f64, 2 v_rsq_f64, 3 v_fma_f32, 4 v_exp_f32), one wave per SIMD.
+//  mfma  Z F32  full-chip MFMA issue rate and the clock the chip holds under it.
+//  kloop V      the fp16x3 layer's K loop alone, with / without its loads.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/ubench tools/ubench.hip
 // Prints one JSON line per case: times from HIP events, cycles from s_memtime
@@ -190,6 +192,191 @@ __global__ __launch_bounds__(64) void lat_bench(int iters, float *out, unsigned 
   if (tid == 0) clk[0] = t1 - t0;
 }
 
+// Full-chip MFMA issue rate (one wave per SIMD, 4 waves per CU, every CU): steps
+// of 96 v_mfma_f32_16x16x32_f16 on 16 accumulators (in-place asm) from register
+// operands, no memory.  Z: operands all zero (1) or
+// random (0): the operand bits set the power drawn.  F32: the fp32 kernel's
+// v_mfma_f32_32x32x2_f32 on 8 accumulators instead (32 per step).
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+template <int Z, int F32>
+__global__ __launch_bounds__(256) void mfma_bench(int iters, float *out, unsigned long long *clk) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const float base = Z ? 0.0f : 0.001f * (tid % 89) + 0.1f;
+  if constexpr (!F32) {
+    h8 a[4], b[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[k][e] = (_Float16)(base * (e + 1) - 0.3f * k);
+        b[k][e] = (_Float16)(base * (7 - e) + 0.2f * k);
+      }
+    f4 c[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) c[q] = f4{0, 0, 0, 0};
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          // (asm: dst = srcC in place; the builtin let the allocator rotate the
+          // accumulators through the loop with ~90 AGPR moves per 96 MFMAs)
+          asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0"
+                       : "+a"(c[q]) : "v"(a[(q + r) & 3]), "v"(b[(q >> 2) & 3]));
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    float acc = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc += (c[q][0] + c[q][1]) + (c[q][2] + c[q][3]);
+    out[tid] = acc;
+    if (tid == 0) clk[0] = t1 - t0;
+  } else {
+    f4 a[2], b[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      a[k] = f4{base, base * 2, base * 3 - 0.1f * k, base * 0.5f};
+      b[k] = f4{base * 5, base - 0.2f * k, base * 0.25f, base * 4};
+    }
+    f16v c[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) c[q][e] = 0.0f;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          c[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[(q + r) & 1][r], b[((q >> 1) + r) & 1][r], c[q], 0, 0, 0);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    float acc = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc += c[q][e];
+    out[tid] = acc;
+    if (tid == 0) clk[0] = t1 - t0;
+  }
+}
+
+// The fp16x3 layer's K loop alone (ik_ann.hip layer_gemm_h16 / step_h16,
+// restated: 4 waves per CU, MR = 2 x NR = 4 tiles of 16x16x32 sub-tiles, the weight
+// stream through a buffer descriptor from a 1 MiB L2-resident operand, a 2-step
+// ring, the activations from LDS split planes, pattern 2), LAYERS x 16 steps with
+// no epilogue: V 0 as production, 1 without the weight loads (the ring's registers
+// reused), 2 without the LDS reads, 3 without either.  cycles per K step per wave.
+typedef float kf4 __attribute__((ext_vector_type(4)));
+struct KSplit2 {
+  h8 hi, lo;
+};
+struct KW {
+  h8 p[4][2][2];  // [tile][feature half][plane]
+};
+constexpr int kKLd = 516;  // floats per LDS row (ik_ann.hip kLd)
+template <int V>
+__global__ __launch_bounds__(256) void kloop_bench(int layers, const h8 *wx, int xbytes,
+                                                   float *out, unsigned long long *clk) {
+  __shared__ float H[64 * kKLd];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 64 * kKLd; i += 256) H[i] = 0.001f * (i % 251);
+  __syncthreads();
+  constexpr int G32 = 16, W = 4;
+  const _Float16 *ap = reinterpret_cast<const _Float16 *>(H + (lane & 15) * kKLd) + 8 * (lane >> 4);
+  const uint64_t bi = reinterpret_cast<uint64_t>(wx);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void *>(bi), 0, xbytes, 0x00020000);
+  int vo[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) vo[j] = ((wave + W * j) * G32 * 4 * 64 + lane) * 16;
+  auto load_w = [&](KW &w, int g) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          w.p[j][fh][p] = __builtin_bit_cast(
+              h8, __builtin_amdgcn_raw_buffer_load_b128(rs, vo[j], (g * 4 + fh * 2 + p) * 1024, 0));
+  };
+  auto load_a = [&](KSplit2 (&a)[2][2], const _Float16 *base, int g) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        const _Float16 *q = base + (m * 32 + 16 * ph) * 2 * kKLd + 32 * g;
+        a[m][ph].hi = *reinterpret_cast<const h8 *>(q);
+        a[m][ph].lo = *reinterpret_cast<const h8 *>(q + 512);
+      }
+  };
+  kf4 acc[2][4][4];
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[m][j][s] = kf4{0, 0, 0, 0};
+  KW w[2];
+  load_w(w[0], 0);
+  load_w(w[1], 1);
+  KSplit2 sa[2][2];
+  load_a(sa, ap, 0);
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int l = 0; l < layers; ++l) {
+    for (int g = 0; g < G32; g += 2) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (V == 0 || V == 2) load_w(w[(u + 1) % 2], g + u + 1);
+        KSplit2 sn[2][2];
+        if (V == 0 || V == 1) load_a(sn, ap + 32 * g, u + 1);
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+              for (int ph = 0; ph < 2; ++ph) {
+                const KW &ww = w[u];
+                kf4 c = acc[m][j][2 * fh + ph];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ww.p[j][fh][0], sa[m][ph].lo, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ww.p[j][fh][1], sa[m][ph].hi, c, 0, 0, 0);
+                acc[m][j][2 * fh + ph] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_f16(ww.p[j][fh][0], sa[m][ph].hi, c, 0, 0, 0);
+              }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (V == 0 || V == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if ((V == 0 || V == 1) && i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (V == 0 || V == 1)
+#pragma unroll
+          for (int m = 0; m < 2; ++m)
+#pragma unroll
+            for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
+      }
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  float r = 0.0f;
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) r += (acc[m][j][q][0] + acc[m][j][q][1]) + (acc[m][j][q][2] + acc[m][j][q][3]);
+  out[blockIdx.x * 256 + threadIdx.x] = r;
+  if (blockIdx.x == 0 && threadIdx.x == 0) clk[0] = t1 - t0;
+}
+
 static int num_cus() {
   int dev = 0, cus = 0;
   CK(hipGetDevice(&dev));
@@ -294,6 +481,59 @@ int main(int argc, char **argv) {
       };
       timed("lat", L, dclk, (double)cus * 4 * 64 * iters, (double)iters, extra);
     }
+  }
+  if (!strcmp(what, "all") || !strcmp(what, "mfma")) {
+    // cycles per MFMA per SIMD (s_memtime) and the clock the chip held (s_memtime
+    // cycles of wave 0 over the launch's event time)
+    // ~40-60 ms per launch (the clock settles under load), each variant twice,
+    // interleaved
+    const int iters = 50000;
+    for (int rep = 0; rep < 2; ++rep)
+    for (int F32 = 0; F32 <= 1; ++F32)
+      for (int Z = 0; Z <= 1; ++Z) {
+        const unsigned blocks = (unsigned)cus;
+        const double per_wave = (double)iters * (F32 ? 32 : 96);
+        snprintf(extra, sizeof extra, "\"instr\": \"%s\", \"zeros\": %d",
+                 F32 ? "v_mfma_f32_32x32x2_f32" : "v_mfma_f32_16x16x32_f16", Z);
+        float *fo = reinterpret_cast<float *>(dout);
+        auto L = [&]() {
+          if (F32) {
+            if (Z) hipLaunchKernelGGL((mfma_bench<1, 1>), dim3(blocks), dim3(256), 0, 0, iters, fo, dclk);
+            else hipLaunchKernelGGL((mfma_bench<0, 1>), dim3(blocks), dim3(256), 0, 0, iters, fo, dclk);
+          } else {
+            if (Z) hipLaunchKernelGGL((mfma_bench<1, 0>), dim3(blocks), dim3(256), 0, 0, iters, fo, dclk);
+            else hipLaunchKernelGGL((mfma_bench<0, 0>), dim3(blocks), dim3(256), 0, 0, iters, fo, dclk);
+          }
+        };
+        timed("mfma", L, dclk, (double)blocks * 4 * per_wave, per_wave, extra);
+      }
+  }
+  if (!strcmp(what, "all") || !strcmp(what, "kloop")) {
+    const int layers = 400;
+    const int xbytes = 16 * 16 * 4 * 1024;  // 16 column tiles x 16 K steps x 4 blocks
+    h8 *wx = nullptr;
+    CK(hipMalloc(&wx, xbytes));
+    {
+      std::vector<_Float16> hw(xbytes / 2);
+      for (size_t i = 0; i < hw.size(); ++i) hw[i] = (_Float16)(0.01f * (float)((i * 37) % 101) - 0.5f);
+      CK(hipMemcpy(wx, hw.data(), xbytes, hipMemcpyHostToDevice));
+    }
+    float *fo = reinterpret_cast<float *>(dout);
+    for (int rep = 0; rep < 2; ++rep)
+      for (int V = 0; V <= 3; ++V) {
+        snprintf(extra, sizeof extra, "\"variant\": %d", V);
+        const double steps = (double)layers * 16;
+        auto L = [&]() {
+          switch (V) {
+            case 0: hipLaunchKernelGGL(kloop_bench<0>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
+            case 1: hipLaunchKernelGGL(kloop_bench<1>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
+            case 2: hipLaunchKernelGGL(kloop_bench<2>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
+            default: hipLaunchKernelGGL(kloop_bench<3>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
+          }
+        };
+        timed("kloop", L, dclk, (double)cus * 4 * steps * 96, steps, extra);  // units: MFMAs
+      }
+    CK(hipFree(wx));
   }
   CK(hipFree(dout));
   CK(hipFree(dgoals));
