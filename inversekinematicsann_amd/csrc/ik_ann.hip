@@ -695,6 +695,9 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
 #define IKHIP_ANN_H16 1
 #endif
 constexpr bool kH16 = IKHIP_ANN_H16 != 0;
+#ifndef IKHIP_ANN_BIAS_FIRST
+#define IKHIP_ANN_BIAS_FIRST 1
+#endif
 // weight-step buffers of the 16x16x32 loop (kH16Ring - 1 steps of 32 ahead)
 #ifndef IKHIP_ANN_H16_RING
 #define IKHIP_ANN_H16_RING 2
@@ -789,6 +792,18 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
                                                const float *bias, f32x16 (&acc)[MR][NR],
                                                unsigned long long *st_first = nullptr) {
   const _Float16 *ap = hplane(const_cast<float *>(H), lane & 15) + 8 * (lane >> 4);
+  // the bias loads go out before the first weight step's: vmcnt counts in issue
+  // order, so the accumulators' start (bias x scale) then waits for the bias
+  // alone and the first MFMAs for their own weight blocks, not for all of the
+  // step's (IKHIP_ANN_BIAS_FIRST)
+  f32x4 bl[NR][2];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh)
+      bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
+                                                   4 * (lane >> 4));
+  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
   WStepH16<NR> w[kH16Ring];
 #pragma unroll
@@ -799,8 +814,7 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
   for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int fh = 0; fh < 2; ++fh) {
-      const f32x4 b = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
-                                                        4 * (lane >> 4)) * scale;
+      const f32x4 b = bl[j][fh] * scale;
 #pragma unroll
       for (int m = 0; m < MR; ++m) c4[m][j][2 * fh] = c4[m][j][2 * fh + 1] = b;
     }
@@ -966,6 +980,14 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
                                                int G32, int xbytes, int wave, int lane,
                                                const float *bias, f32x16 (&acc)[MR][NR]) {
   const float *ap = H + (lane & 15) * kLd + 8 * (lane >> 4);
+  f32x4 bl[NR][2];  // before the weights (layer_gemm_h16)
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh)
+      bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
+                                                   4 * (lane >> 4));
+  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 6, lane);
   WStepX16<NR> w[2];
   load_wx16(w[0], ws, 0);
@@ -974,8 +996,7 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
   for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int fh = 0; fh < 2; ++fh) {
-      const f32x4 b = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
-                                                        4 * (lane >> 4));
+      const f32x4 b = bl[j][fh];
 #pragma unroll
       for (int m = 0; m < MR; ++m) c4[m][j][2 * fh] = c4[m][j][2 * fh + 1] = b;
     }
