@@ -124,12 +124,16 @@ __device__ __forceinline__ f32x2 act_apply2(f32x2 v) {
 
 // Four pairs at once, phase by phase (see layer_store): the dependent exp / rcp
 // chains of the eight elements overlap.
+// pre: a power-of-two scale still to be applied to v (the fp16x3 weight
+// pre-scale, 1 elsewhere); for tanh it folds into exp2's argument scale, which
+// rounds the same way (pre * 2 log2(e) is exact, and v * pre would be).
 template <int ACT>
-__device__ __forceinline__ void act_apply2x4(f32x2 (&v)[4]) {
+__device__ __forceinline__ void act_apply2x4(f32x2 (&v)[4], float pre = 1.0f) {
   if constexpr (ACT == IK_ACT_TANH) {
     f32x2 e[4];
+    const float k2 = 2.885390081777927f * pre;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) e[k] = v[k] * 2.885390081777927f;
+    for (int k = 0; k < 4; ++k) e[k] = v[k] * k2;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       e[k].x = __builtin_amdgcn_exp2f(e[k].x);
@@ -147,7 +151,7 @@ __device__ __forceinline__ void act_apply2x4(f32x2 (&v)[4]) {
       v[k] = __builtin_elementwise_fma(e[k], f32x2{-2.0f, -2.0f}, f32x2{1.0f, 1.0f});
   } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v[k] = act_apply2<ACT>(v[k]);
+    for (int k = 0; k < 4; ++k) v[k] = act_apply2<ACT>(v[k] * pre);
   }
 }
 
@@ -842,7 +846,8 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) acc[m][j][4 * s + i] = c4[m][j][s][i] * xinv;
+        for (int i = 0; i < 4; ++i) acc[m][j][4 * s + i] = c4[m][j][s][i];
+  (void)xinv;  // the epilogue applies it (layer_store_h16's pre)
 }
 
 // Epilogue of an fp16x3 layer in the 16x16 sub-tile layout above: per lane and
@@ -850,7 +855,8 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
 // (or one ds_write_b128 of fp32).
 template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
 __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
-                                                f32x16 (&acc)[MR][NR], unsigned long long *st) {
+                                                f32x16 (&acc)[MR][NR], unsigned long long *st,
+                                                float pre = 1.0f) {
   stamp(st);
   __syncthreads();  // every wave has finished reading the layer input
 #pragma unroll
@@ -866,7 +872,7 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
           const int q = 4 * (2 * fh + (k >> 1)) + 2 * (k & 1);
           t[k] = f32x2{acc[m][j][q], acc[m][j][q + 1]};
         }
-        act_apply2x4<ACT>(t);
+        act_apply2x4<ACT>(t, pre);
 #pragma unroll
         for (int ph = 0; ph < 2; ++ph) {
           const int row = m * 32 + 16 * ph + (lane & 15);
@@ -1033,25 +1039,27 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
 template <int ACT, bool HOUT, int W, int X, int MR, int NR>
 __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[NR], int wave,
                                           int lane, f32x16 (&acc)[MR][NR],
-                                          unsigned long long *st) {
+                                          unsigned long long *st, float pre) {
   if (tr) {
     if constexpr ((X == 2 && kH16) || (X == 1 && kX16))
-      layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
+      layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st, pre);
     else layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
   } else {
     layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
   }
 }
 
+// pre: the fp16x3 16x16x32 GEMM's accumulators still carry the weight pre-scale
+// (layer_gemm_h16); 1 for every other layer.
 template <bool HOUT, int W, int X, int MR, int NR>
 __device__ __forceinline__ void store_act(int act, bool tr, float *H, const float (&bv)[NR],
                                           int wave, int lane, f32x16 (&acc)[MR][NR],
-                                          unsigned long long *st) {
+                                          unsigned long long *st, float pre = 1.0f) {
   switch (act) {
-    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
-    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
-    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
-    default: store_any<IK_ACT_LINEAR, HOUT, W, X>(tr, H, bv, wave, lane, acc, st); break;
+    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    default: store_any<IK_ACT_LINEAR, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
   }
 }
 
@@ -1085,8 +1093,9 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
     for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + W * j) * 32 + (lane & 31)];
     layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, W, lane, nullptr, acc, st_first);
   }
-  if (HX && hout) store_act<true, W, X>(act, tr, H, bv, wave, lane, acc, st);
-  else store_act<false, W, X>(act, tr, H, bv, wave, lane, acc, st);
+  const float pre = (X == 2 && kH16 && tr) ? xinv : 1.0f;
+  if (HX && hout) store_act<true, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
+  else store_act<false, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
 }
 
 // HOUT: the next layer runs fp16x3, so the result goes out as split planes

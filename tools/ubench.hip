@@ -12,7 +12,8 @@
 //  lat   K      dependent-chain latency of one instruction kind (K 0 v_fma_f64,
 //               1 v_rcp_f64, 2 v_rsq_f64, 3 v_fma_f32, 4 v_exp_f32), one wave per SIMD.
 //  mfma  Z F32  full-chip MFMA issue rate and the clock the chip holds under it.
-//  kloop V      the fp16x3 layer's K loop alone, with / without its loads.
+//  kloop V      the fp16x3 layer's K loop alone, with / without its loads, and over
+//               a 12 MiB weight set (V 4; V 5 with each workgroup at its own layer).
 //
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -o tools/ubench tools/ubench.hip
 // Prints one JSON line per case: times from HIP events, cycles from s_memtime
@@ -278,8 +279,11 @@ struct KW {
   h8 p[4][2][2];  // [tile][feature half][plane]
 };
 constexpr int kKLd = 516;  // floats per LDS row (ik_ann.hip kLd)
+// V 4: as V 0, but layer l reads weight slice l % 12 of a 12 MiB operand (the
+// reference model's 11 hidden layers do not fit one XCD's 4 MB L2); V 5: each
+// workgroup starts at its own slice (blockIdx % 12), as drifted workgroups are.
 template <int V>
-__global__ __launch_bounds__(256) void kloop_bench(int layers, const h8 *wx, int xbytes,
+__global__ __launch_bounds__(256) void kloop_bench(int layers, const h8 *wx0, int xbytes,
                                                    float *out, unsigned long long *clk) {
   __shared__ float H[64 * kKLd];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -287,9 +291,8 @@ __global__ __launch_bounds__(256) void kloop_bench(int layers, const h8 *wx, int
   __syncthreads();
   constexpr int G32 = 16, W = 4;
   const _Float16 *ap = reinterpret_cast<const _Float16 *>(H + (lane & 15) * kKLd) + 8 * (lane >> 4);
-  const uint64_t bi = reinterpret_cast<uint64_t>(wx);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void *>(bi), 0, xbytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<h8 *>(wx0), 0, xbytes, 0x00020000);
   int vo[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) vo[j] = ((wave + W * j) * G32 * 4 * 64 + lane) * 16;
@@ -327,13 +330,17 @@ __global__ __launch_bounds__(256) void kloop_bench(int layers, const h8 *wx, int
   load_a(sa, ap, 0);
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int l = 0; l < layers; ++l) {
+    if (V >= 4) {  // 5: each workgroup at its own layer phase (blockIdx % 12)
+      const h8 *wl = wx0 + (size_t)((l + (V == 5 ? blockIdx.x : 0)) % 12) * (xbytes / 16);
+      rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<h8 *>(wl), 0, xbytes, 0x00020000);
+    }
     for (int g = 0; g < G32; g += 2) {
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         __builtin_amdgcn_sched_barrier(0);
-        if (V == 0 || V == 2) load_w(w[(u + 1) % 2], g + u + 1);
+        if (V == 0 || V == 2 || V >= 4) load_w(w[(u + 1) % 2], g + u + 1);
         KSplit2 sn[2][2];
-        if (V == 0 || V == 1) load_a(sn, ap + 32 * g, u + 1);
+        if (V == 0 || V == 1 || V >= 4) load_a(sn, ap + 32 * g, u + 1);
 #pragma unroll
         for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -351,13 +358,13 @@ __global__ __launch_bounds__(256) void kloop_bench(int layers, const h8 *wx, int
               }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          if (V == 0 || V == 2) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          if (V == 0 || V == 2 || V >= 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if ((V == 0 || V == 1) && i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if ((V == 0 || V == 1 || V >= 4) && i < 8) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
           __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (V == 0 || V == 1)
+        if (V == 0 || V == 1 || V >= 4)
 #pragma unroll
           for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -512,15 +519,15 @@ int main(int argc, char **argv) {
     const int layers = 400;
     const int xbytes = 16 * 16 * 4 * 1024;  // 16 column tiles x 16 K steps x 4 blocks
     h8 *wx = nullptr;
-    CK(hipMalloc(&wx, xbytes));
+    CK(hipMalloc(&wx, (size_t)xbytes * 12));
     {
-      std::vector<_Float16> hw(xbytes / 2);
+      std::vector<_Float16> hw((size_t)xbytes * 12 / 2);
       for (size_t i = 0; i < hw.size(); ++i) hw[i] = (_Float16)(0.01f * (float)((i * 37) % 101) - 0.5f);
-      CK(hipMemcpy(wx, hw.data(), xbytes, hipMemcpyHostToDevice));
+      CK(hipMemcpy(wx, hw.data(), (size_t)xbytes * 12, hipMemcpyHostToDevice));
     }
     float *fo = reinterpret_cast<float *>(dout);
     for (int rep = 0; rep < 2; ++rep)
-      for (int V = 0; V <= 3; ++V) {
+      for (int V = 0; V <= 5; ++V) {
         snprintf(extra, sizeof extra, "\"variant\": %d", V);
         const double steps = (double)layers * 16;
         auto L = [&]() {
@@ -528,7 +535,9 @@ int main(int argc, char **argv) {
             case 0: hipLaunchKernelGGL(kloop_bench<0>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
             case 1: hipLaunchKernelGGL(kloop_bench<1>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
             case 2: hipLaunchKernelGGL(kloop_bench<2>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
-            default: hipLaunchKernelGGL(kloop_bench<3>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
+            case 3: hipLaunchKernelGGL(kloop_bench<3>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
+            case 4: hipLaunchKernelGGL(kloop_bench<4>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
+            default: hipLaunchKernelGGL(kloop_bench<5>, dim3(cus), dim3(256), 0, 0, layers, wx, xbytes, fo, dclk); break;
           }
         };
         timed("kloop", L, dclk, (double)cus * 4 * steps * 96, steps, extra);  // units: MFMAs
