@@ -283,6 +283,43 @@ def test_ann_tanh_accuracy(ctx1, hidden):
     assert np.array_equal(ang[:, :3][big], np.sign(pts[big]).astype(np.float32))
 
 
+@pytest.mark.parametrize("hidden", [True, False])
+def test_ann_sigmoid_accuracy(ctx1, hidden):
+    """The kernels' sigmoid (1 / (1 + exp2(-log2(e) v)), hardware exp2 and
+    reciprocal) against float64: absolute error <= 2e-7 everywhere over [-90, 90];
+    relative error <= 4 fp32 ulps (4.8e-7) plus the exponent argument's own fp32
+    rounding, which exp2 turns into a relative error of up to |v| log2(e) 2^-24 ln 2
+    (bounded here by 9e-8 |v|), wherever the value is >= 1e-30; exactly 0.5 at 0 and 1
+    in saturation.  Same identity-weight models as the tanh test."""
+    rng = np.random.default_rng(5)
+    n = 20_000
+    pts = np.concatenate([rng.uniform(-90, 90, (n, 3)), rng.uniform(-20, 20, (n, 3)),
+                          np.array([[0.0, -0.0, 200.0], [-200.0, 1e-30, 17.0]])])
+    if hidden:
+        W1 = np.zeros((3, 32), np.float32)
+        W1[0, 0] = W1[1, 1] = W1[2, 2] = 1.0
+        W2 = np.zeros((32, 4), np.float32)
+        W2[0, 0] = W2[1, 1] = W2[2, 2] = 1.0
+        Ws, bs, acts = [W1, W2], [np.zeros(32, np.float32), np.zeros(4, np.float32)], \
+            ["sigmoid", "linear"]
+    else:
+        W = np.zeros((3, 4), np.float32)
+        W[0, 0] = W[1, 1] = W[2, 2] = 1.0
+        Ws, bs, acts = [W], [np.zeros(4, np.float32)], ["sigmoid"]
+    ctx1.ann_load(Ws, bs, acts, np.zeros(3), np.ones(3), np.zeros(4), np.ones(4))
+    ang, _, _ = ctx1.ann_solve(pts, check_limits=False)
+    x = pts.astype(np.float32).astype(np.float64)
+    ref = 1.0 / (1.0 + np.exp(-x))
+    got = ang[:, :3].astype(np.float64)
+    assert np.abs(got - ref).max() <= 2e-7, float(np.abs(got - ref).max())
+    big = ref >= 1e-30
+    rel = np.abs(got[big] - ref[big]) / ref[big]
+    bound = 4.8e-7 + 9e-8 * np.abs(x[big])
+    assert np.all(rel <= bound), float((rel / bound).max())
+    assert got[pts[:, :3] == 0.0].tolist() == [0.5] * int((pts[:, :3] == 0.0).sum())
+    assert np.all(got[pts[:, :3] >= 200.0] == 1.0)
+
+
 def test_ann_width_cap(ctx1):
     """ik_ann_load takes widths up to 1024 and refuses only wider layers."""
     from inversekinematicsann_amd import _native
