@@ -491,6 +491,9 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 // distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
 // Every solve reaching this kernel runs at least one iteration (the host sends
 // the others to fabrik_simple_kernel), so the seed's last joint is never needed.
+#ifndef IKHIP_FAB_INNER  // 1: the iterations in a loop of their own inside the refill loop
+#define IKHIP_FAB_INNER 1
+#endif
 #ifndef IKHIP_ITER_WAVES
 #define IKHIP_ITER_WAVES 2
 #endif
@@ -700,6 +703,13 @@ fabrik_iter_kernel(FabArgs a) {
       dry = nstage < 0 && pptr >= pcount;
       IKHIP_DT_ACC(kDiagRefillTicks, kDiagTRefill);
     }
+#if IKHIP_FAB_INNER
+    // iterate until a refill is due (REFILL_MIN lanes free) or, once the queue is
+    // dry, until every lane has stopped: the refill's scalar state stays out of
+    // this loop, so its SGPRs are not reloaded from their spill lanes per iteration
+    const int need = dry ? 64 : REFILL_MIN;
+    while (true) {
+#endif
 #ifdef IKHIP_DIAG
     {
       const unsigned long long sm =
@@ -719,6 +729,9 @@ fabrik_iter_kernel(FabArgs a) {
       const bool run = active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step);
       pending = pending || (active && !run);
       active = run;
+#if IKHIP_FAB_INNER
+      if (__popcll(__ballot(!run)) >= need) break;
+#endif
       if (run) {
         if constexpr (CORE == 2) {
           uint32_t dom = 0, cdom_n = cdom;
@@ -759,6 +772,9 @@ fabrik_iter_kernel(FabArgs a) {
         ++step;
       }
     }
+#if IKHIP_FAB_INNER
+    }
+#endif
   }
   // drain: park the last finished lanes, then the angles step on the ring
   IKHIP_DT(kDiagTDrain);
