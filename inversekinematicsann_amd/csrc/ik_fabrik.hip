@@ -166,7 +166,7 @@ enum { kDiagLoops, kDiagSteps, kDiagLaneSteps, kDiagRefills, kDiagGrabs, kDiagFa
        kDiagParkTicks, kDiagStageTicks, kDiagCount };
 // per-wave record (kDiagWords): the counters above, then s_memrealtime stamps
 enum { kDiagTStart = kDiagCount, kDiagTDry, kDiagTLast, kDiagStepsDry, kDiagTDrain, kDiagTEnd,
-       kDiagTRefill, kDiagTSub, kDiagWords = 24 };
+       kDiagTRefill, kDiagTSub, kDiagDrainN, kDiagTDrain2, kDiagWords = 24 };
 #ifdef IKHIP_DIAG
 constexpr int kDiagWaveMax = 4096;  // = (kFabrikDebugWords - 64) / kDiagWords (24)
 #endif
@@ -464,9 +464,28 @@ __device__ __forceinline__ void ring_put(RetireRing &R, int s, const d3 &J0, con
 
 // The angles step over the ring's first cnt entries (the whole wave calls it).
 // ORD: 1 in kOrdSample points records (cell, iterations) for the cost table.
+// IKHIP_FAB_PRIO: the angles step and the seed preparation run at a raised wave
+// priority.  Two waves share a SIMD and, at equal priority, the older one's VALU
+// wins every issue arbitration (MI355X_MICROARCH.md, "Two waves per SIMD"): a
+// younger wave's angles step -- long dependent chains, few instructions ready at
+// a time -- then gets only the slots its iterating partner leaves and took 10-50 us
+// instead of 2.5 for one wave in ten at the end of the launch.  Raised, it issues
+// whenever it has an instruction ready and the partner's issue-bound iteration
+// fills the rest.
+#ifndef IKHIP_FAB_PRIO
+#define IKHIP_FAB_PRIO 2
+#endif
+__device__ __forceinline__ void prio_raise() {
+  if (IKHIP_FAB_PRIO) __builtin_amdgcn_s_setprio(IKHIP_FAB_PRIO);
+}
+__device__ __forceinline__ void prio_drop() {
+  if (IKHIP_FAB_PRIO) __builtin_amdgcn_s_setprio(0);
+}
+
 template <bool ORD>
 __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int cnt, int lane,
                                            LaneAcc &acc) {
+  prio_raise();
   __builtin_amdgcn_wave_barrier();
   if (lane < cnt) {
     d3 J[4];
@@ -483,6 +502,7 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
     }
   }
   __builtin_amdgcn_wave_barrier();
+  prio_drop();
 }
 
 
@@ -661,6 +681,7 @@ fabrik_iter_kernel(FabArgs a) {
           pcount = ncount;
           pptr = 0;
           nstage = 0;
+          prio_raise();
           if (lane < pcount) {
             const RcConst k = opaque_rc(a.rc);
             if (a.check_limits && outside_rc(k, ng))
@@ -673,6 +694,7 @@ fabrik_iter_kernel(FabArgs a) {
             PB.v[9][lane] = ng.x; PB.v[10][lane] = ng.y; PB.v[11][lane] = ng.z;
             PB.idx[lane] = ni;
           }
+          prio_drop();
 #ifdef IKHIP_DIAG
           // (the seed's loads are consumed before the stamp)
           __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the batch's LDS writes landed
@@ -781,10 +803,12 @@ fabrik_iter_kernel(FabArgs a) {
   {
     const unsigned long long pm = __ballot(pending);
     const int np = __popcll(pm);
+    IKHIP_DG(kDiagDrainN, rcnt + np);
     if (rcnt + np > 64) {
       ring_flush<ORD>(a, R, rcnt, lane, acc);
       rcnt = 0;
     }
+    IKHIP_DT(kDiagTDrain2);
     if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, g, out, step, st);
     rcnt += np;
     IKHIP_DG(kDiagFlushes, 1);

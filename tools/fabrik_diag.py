@@ -60,6 +60,39 @@ for tol, mi in ((1e-3, 100), (1e-5, 200)):
     c["last_step_to_drain_us"] = span(TLAST, TDRAIN)
     c["drain_to_end_us"] = span(TDRAIN, TEND)
     c["wave_us"] = span(T0, TEND)
+    # the drain: entries parked + flushed at the end, the optional first flush
+    # (ring overflow) and the final one; the slowest 10 % of drains against the rest
+    DRAINN, TDRAIN2 = T0 + 8, T0 + 9
+    dn = t[:, DRAINN]
+    d1 = (t[:, TDRAIN2] - t[:, TDRAIN]) / 100.0
+    d2 = (t[:, TEND] - t[:, TDRAIN2]) / 100.0
+    dd = (t[:, TEND] - t[:, TDRAIN]) / 100.0
+    slow = dd >= np.percentile(dd, 90)
+    c["drain_entries"] = np.percentile(dn, pc).tolist()
+    c["drain_first_flush_us"] = np.percentile(d1, pc).round(2).tolist()
+    c["drain_final_flush_us"] = np.percentile(d2, pc).round(2).tolist()
+    c["drain_slow10"] = {"entries_median": float(np.median(dn[slow])),
+                         "entries_median_rest": float(np.median(dn[~slow])),
+                         "first_us_median": float(np.median(d1[slow])),
+                         "final_us_median": float(np.median(d2[slow])),
+                         "dry_us_median": float(np.median((t[slow, TDRY] - t0) / 100.0)),
+                         "dry_us_median_rest": float(np.median((t[~slow, TDRY] - t0) / 100.0)),
+                         "slot_in_block": np.bincount(np.arange(nw)[slow] % 4, minlength=4).tolist()}
+    # block-mates (same CU) already finished when a wave's drain starts
+    blk = np.arange(nw) // 4
+    mates_done = np.array([int(((blk == blk[w]) & (t[:, TEND] < t[w, TDRAIN])).sum())
+                           for w in range(nw)])
+    c["drain_slow10"]["mates_done_hist"] = np.bincount(mates_done[slow], minlength=4).tolist()
+    c["drain_rest_mates_done_hist"] = np.bincount(mates_done[~slow], minlength=4).tolist()
+    # by XCD (blocks are dealt round-robin over the 8 XCDs; 4 waves per block):
+    # median dry / end time, to tell clock domains from backlogs
+    xcd = (np.arange(nw) // 4) % 8
+    c["dry_us_by_xcd"] = [round(float(np.median((t[xcd == x, TDRY] - t0) / 100.0)), 1)
+                          for x in range(8)]
+    c["end_us_by_xcd"] = [round(float(np.median((t[xcd == x, TEND] - t0) / 100.0)), 1)
+                          for x in range(8)]
+    c["end_p99_us_by_xcd"] = [round(float(np.percentile((t[xcd == x, TEND] - t0) / 100.0, 99)), 1)
+                              for x in range(8)]
     # busy waves over time (10 us bins): how the launch drains
     edges = np.arange(0, (t[:, TEND].max() - t0) / 100.0 + 10, 10)
     c["waves_running_10us"] = [int(((t[:, T0] - t0) / 100.0 <= e).sum() -
