@@ -166,7 +166,7 @@ enum { kDiagLoops, kDiagSteps, kDiagLaneSteps, kDiagRefills, kDiagGrabs, kDiagFa
        kDiagParkTicks, kDiagStageTicks, kDiagCount };
 // per-wave record (kDiagWords): the counters above, then s_memrealtime stamps
 enum { kDiagTStart = kDiagCount, kDiagTDry, kDiagTLast, kDiagStepsDry, kDiagTDrain, kDiagTEnd,
-       kDiagTRefill, kDiagTSub, kDiagDrainN, kDiagTDrain2, kDiagWords = 24 };
+       kDiagTRefill, kDiagTSub, kDiagDrainN, kDiagTDrain2, kDiagHwId, kDiagWords = 24 };
 #ifdef IKHIP_DIAG
 constexpr int kDiagWaveMax = 4096;  // = (kFabrikDebugWords - 64) / kDiagWords (24)
 #endif
@@ -577,6 +577,10 @@ fabrik_iter_kernel(FabArgs a) {
   if (lane < kDiagWords) dg[lane] = 0;
   __builtin_amdgcn_wave_barrier();
   if (lane == 0) dg[kDiagTStart] = __builtin_amdgcn_s_memrealtime();
+  // where the wave runs: XCC_ID (hwreg 20) << 32 | HW_ID (hwreg 4: wave 3:0, SIMD 5:4, CU 11:8, SE 14:13)
+  if (lane == 0)
+    dg[kDiagHwId] = ((unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32) |
+                    (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);
 #define IKHIP_DG(k, v) \
   do {                 \
     if (lane == 0) dg[k] += (v); \
@@ -833,12 +837,19 @@ fabrik_iter_kernel(FabArgs a) {
   if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
   if constexpr (ORD) {
     // the last block to finish folds this call's records into the cost table
-    // (the next call's classify reads it); every thread fences its sample stores
+    // (the next call's classify reads it).  Publishing the sample stores: each wave
+    // waits for its own stores to reach L2 (vmcnt(0)), then ONE agent-scope release
+    // per block (buffer_wbl2: the XCD's L2 written back) before the ticket.  With a
+    // __threadfence in every wave, 2048 L2 write-backs ran while the last waves
+    // were still draining and stretched their angles steps from ~2.5 us to 10-50 us
+    // (tools/fabrik_diag.py: slow drains while 20-80 % of the waves had ended).
     __shared__ int last;
-    __threadfence();
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __syncthreads();
-    if (threadIdx.x == 0)
+    if (threadIdx.x == 0) {
+      __threadfence();
       last = atomicAdd(&a.S->ticket, 1ull) == (unsigned long long)(gridDim.x - 1);
+    }
     __syncthreads();
     if (last) {
       __threadfence();

@@ -39,6 +39,8 @@ for tol, mi in ((1e-3, 100), (1e-5, 200)):
     # dry, drain, end (s_memrealtime, 100 MHz)
     T0, TDRY, TLAST, SDRY, TDRAIN, TEND = range(len(NAMES), len(NAMES) + 6)
     t0 = t[:, T0].min()
+    if os.environ.get("FABRIK_DIAG_RAW"):  # the per-wave records, for offline analysis
+        np.save(os.path.join(os.environ["FABRIK_DIAG_RAW"], f"fabrik_diag_raw_tol{tol:g}.npy"), t)
     pc = [0, 1, 10, 50, 90, 99, 100]
     us = lambda v: np.percentile((v - t0) / 100.0, pc).round(1).tolist()
     span = lambda a, b: np.percentile((t[:, b] - t[:, a]) / 100.0, pc).round(2).tolist()
