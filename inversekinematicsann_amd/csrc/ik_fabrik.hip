@@ -835,28 +835,18 @@ fabrik_iter_kernel(FabArgs a) {
 #undef IKHIP_DT_ACC
   block_iter_stats_acc(a.S, acc.sum_it, acc.capped, acc.max_it);
   if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
-  if constexpr (ORD) {
-    // the last block to finish folds this call's records into the cost table
-    // (the next call's classify reads it).  Publishing the sample stores: each wave
-    // waits for its own stores to reach L2 (vmcnt(0)), then ONE agent-scope release
-    // per block (buffer_wbl2: the XCD's L2 written back) before the ticket.  With a
-    // __threadfence in every wave, 2048 L2 write-backs ran while the last waves
-    // were still draining and stretched their angles steps from ~2.5 us to 10-50 us
-    // (tools/fabrik_diag.py: slow drains while 20-80 % of the waves had ended).
-    __shared__ int last;
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __threadfence();
-      last = atomicAdd(&a.S->ticket, 1ull) == (unsigned long long)(gridDim.x - 1);
-    }
-    __syncthreads();
-    if (last) {
-      __threadfence();
-      const int64_t ns = (a.n + kOrdSample - 1) / kOrdSample;
-      order_fold(a.ord, (unsigned int)(ns < kOrdMaxSample ? ns : kOrdMaxSample));
-    }
-  }
+  // (ORD: the cost table is folded by fabrik_fold_kernel, launched next on the
+  // same stream: the kernel boundary publishes the sample stores, so no block
+  // fences them here -- a release per wave, and later one per block, wrote the
+  // XCD's L2 back while the last waves were still draining, r03)
+}
+
+// The cost-table fold after an ordered solve (one block): this call's samples
+// (the retire steps' stores, published by the kernel boundary) into the table
+// the next call's classify reads.
+__global__ __launch_bounds__(256) void fabrik_fold_kernel(FabArgs a) {
+  const int64_t ns = (a.n + kOrdSample - 1) / kOrdSample;
+  order_fold(a.ord, (unsigned int)(ns < kOrdMaxSample ? ns : kOrdMaxSample));
 }
 
 static size_t up256(size_t b) { return (b + 255) & ~(size_t)255; }
@@ -988,6 +978,11 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     else launch_iter<8, false>(core, pgrid, stream, a);
   }
   kt_end(stream);
+  if (ordered) {
+    kt_begin("fabrik_fold_kernel", stream);
+    hipLaunchKernelGGL(fabrik_fold_kernel, dim3(1), dim3(256), 0, stream, a);
+    kt_end(stream);
+  }
 }
 
 // ------------------------------------------------------ Fabrik.calculate ----

@@ -43,6 +43,7 @@ METHODS_OF = {"ann_fused_kernel": ["ann"],
               "fabrik_classify_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fabrik_scatter_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fabrik_iter_kernel": ["fabrik", "fabrik_tol1e-5"],
+              "fabrik_fold_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fk_kernel": ["fk"]}
 
 
