@@ -35,7 +35,7 @@ constexpr int kQueueHeads = 8;
 struct DevStats {
   unsigned long long first_oob;      // atomicMin of point index
   unsigned long long first_err_key;  // atomicMin of (index << 8) | code
-  unsigned long long ticket;         // blocks of the FABRIK iteration kernel that finished
+  unsigned long long ticket;         // unused since r03 (the FABRIK fold is its own kernel); kept for the layout
   // FABRIK work order: points per (cost class, block shard), and the scatter's
   // cursor inside each (class, shard) region of the queue
   unsigned int cls_tot[kOrdClasses][kOrdShards];
