@@ -343,19 +343,12 @@ __device__ __forceinline__ void store_h1(float *H, int row, int col, float v) {
 // transposed form below (bias in the accumulators, b128 stores) measured
 // 0.6 k cycles per layer slower here: its 5.9 k-cycle epilogue saves 0.7 k,
 // its GEMM loses 1.3 k (bias loads ahead of the first MFMA).
-// IKHIP_ANN_EPI_PRIO (A/B knob, 0 = off): the epilogue at a raised wave priority, so
-// that at two workgroups per CU it is not left the issue slots of the partner
-// wave's K loop (MI355X_MICROARCH.md, "Two waves per SIMD").
-#ifndef IKHIP_ANN_EPI_PRIO
-#define IKHIP_ANN_EPI_PRIO 0
-#endif
 template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
 __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], int wave, int lane,
                                               f32x16 (&acc)[MR][NR], unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
   stamp(st);
   __syncthreads();  // every wave has finished reading the layer input
-  if (IKHIP_ANN_EPI_PRIO) __builtin_amdgcn_s_setprio(IKHIP_ANN_EPI_PRIO);
 #pragma unroll
   for (int j = 0; j < NR; ++j) {
     const int col = (wave + W * j) * 32 + r;
@@ -382,7 +375,6 @@ __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], i
         }
       }
   }
-  if (IKHIP_ANN_EPI_PRIO) __builtin_amdgcn_s_setprio(0);
 }
 
 // Epilogue of a full-width split-mode layer on the transposed tile (mma_group TR): the
