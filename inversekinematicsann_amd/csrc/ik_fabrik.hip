@@ -511,6 +511,9 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 // distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
 // Every solve reaching this kernel runs at least one iteration (the host sends
 // the others to fabrik_simple_kernel), so the seed's last joint is never needed.
+#ifndef IKHIP_FAB_REFILL  // free lanes that trigger a refill (r01: 8 against 4 / 16)
+#define IKHIP_FAB_REFILL 8
+#endif
 #ifndef IKHIP_FAB_INNER  // 1: the iterations in a loop of their own inside the refill loop
 #define IKHIP_FAB_INNER 1
 #endif
@@ -974,8 +977,8 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     if (ordered) launch_iter<1, true>(core, pgrid, stream, a);
     else launch_iter<1, false>(core, pgrid, stream, a);
   } else {
-    if (ordered) launch_iter<8, true>(core, pgrid, stream, a);
-    else launch_iter<8, false>(core, pgrid, stream, a);
+    if (ordered) launch_iter<IKHIP_FAB_REFILL, true>(core, pgrid, stream, a);
+    else launch_iter<IKHIP_FAB_REFILL, false>(core, pgrid, stream, a);
   }
   kt_end(stream);
   if (ordered) {
