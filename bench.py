@@ -85,6 +85,10 @@ def maybe_launch(argv=None):
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ)
+    # the ranks' runtime must use dmabuf IPC: this pool's host driver
+    # supports only that, and RCCL's peer setup fails with hipIpcGetMemHandle:
+    # invalid argument under the legacy mode; the pool already exports it, and an
+    # explicit value in the environment wins
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(launch_command(argv, gpus, port), env=env)
 
@@ -140,8 +144,11 @@ def dist_setup(args):
         local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if "WORLD_SIZE" in os.environ:  # launched by torch.distributed.run (any N)
+        import datetime
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        # a bounded control plane too: a rank that never reaches a barrier ends
+        # the run instead of holding it to the driver's limit
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=600))
     return world, rank, local
 
 
@@ -275,6 +282,69 @@ def _own_parts(job):
     return [D.part_bounds(job.total, job.world, max(1, chunks), job.sc.rank, c) for c in range(C)]
 
 
+def _check_parts(job):
+    """The rows this rank re-solves after a sharded step: the first and the last
+    part of rank (r + 1) % N in the plan the library used (ik_comm_info)."""
+    from inversekinematicsann_amd import dist as D
+    q = (job.sc.rank + 1) % job.world
+    chunks = max(1, job.sc.info()[2])
+    C, _, _ = D.plan_of(job.total, job.world, chunks)
+    parts = [D.part_bounds(job.total, job.world, chunks, q, c) for c in range(C)]
+    parts = [p for p in parts if p[1] > p[0]]
+    return sorted({parts[0], parts[-1]}) if parts else []
+
+
+def _as_bytes(x):
+    if hasattr(x, "detach"):
+        x = x.detach().cpu().numpy()
+    x = np.ascontiguousarray(x)
+    return x.view(np.uint8).reshape(x.shape[0], -1) if x.ndim else x.view(np.uint8)
+
+
+def compare_rows(gathered, resolved):
+    """Bit-for-bit comparison of gathered rows with a plain re-solve of the same
+    rows: {output name: array} each.  Returns (rows, mismatching rows)."""
+    rows, bad = 0, 0
+    for k, ref in resolved.items():
+        a, b = _as_bytes(gathered[k]), _as_bytes(ref)
+        if a.shape != b.shape:
+            return max(rows, b.shape[0]), b.shape[0]
+        diff = (a != b).reshape(a.shape[0], -1).any(axis=1)
+        rows = max(rows, a.shape[0])
+        bad = max(bad, int(diff.sum()))
+    return rows, bad
+
+
+def gather_check(job, outputs, resolve):
+    """N > 1: after the timed steps each rank re-solves, plainly
+    and unsharded, rank (r + 1) % N's first and last parts of the batch and
+    compares them bit for bit with what the all-gather delivered into its own
+    arrays (angles, and FABRIK's iteration counts).  Row counts add up and the
+    verdict is AND-reduced over the ranks; None without a sharded context."""
+    if job.sc is None:
+        return None
+    rows, bad = 0, 0
+    for b, e in _check_parts(job):
+        r, x = compare_rows({k: v[b:e] for k, v in outputs.items()}, resolve(b, e))
+        rows, bad = rows + r, bad + x
+    rows = int(sum_over_ranks(rows, job.world))
+    bad = int(sum_over_ranks(bad, job.world))
+    return {"rows": rows, "mismatched_rows": bad, "bit_exact": bad == 0,
+            "what": "every rank re-solved rank (r+1)%N's first and last parts unsharded and "
+                    "compared them bit for bit with its gathered rows"}
+
+
+def gather_verdict(checks):
+    """The line's config.gather_check from the methods' checks, and the exit code:
+    0, or 3 when any gathered row differs from its re-solve."""
+    checks = {k: v for k, v in checks.items() if v}
+    if not checks:
+        return None, 0
+    ok = all(v["bit_exact"] for v in checks.values())
+    return ({"rows": sum(v["rows"] for v in checks.values()), "bit_exact": ok,
+             "per_method": checks}, 0 if ok else 3)
+
+
 def _p99(job, derr, world):
     """p99 of the FK errors: after a sharded step the library's gathered
     histograms (every rank's own rows; an upper bound within 1/16 octave), else
@@ -351,6 +421,13 @@ def run_ann(job, args, mode="fp32"):
     if job.sc is not None:
         res["gather_chunks"] = job.sc.info()[2]
         res["gather_ms"] = st.gather_ms
+
+        def resolve(b, e):
+            a = torch.empty((e - b, 4), dtype=torch.float32, device="cuda")
+            ctx.ann_solve_device(job.dpts[b:e], a, torch.empty(e - b, dtype=torch.float64,
+                                                               device="cuda"))
+            return {"ang": a}
+        res["gather_check"] = gather_check(job, {"ang": dang}, resolve)
     mx, sm, _, _ = _stats_over_ranks(job, st, res)
     res["max_fk_err"] = mx
     res["mean_fk_err"] = sm / job.total
@@ -420,6 +497,14 @@ def run_fabrik(job, args, tol=None, max_iter=None):
     if job.sc is not None:
         res["gather_chunks"] = job.sc.info()[2]
         res["gather_ms"] = st.gather_ms
+
+        def resolve(b, e):
+            a = torch.empty((e - b, 4), dtype=torch.float64, device="cuda")
+            i = torch.empty(e - b, dtype=torch.int32, device="cuda")
+            ctx.fabrik_solve_device(job.dpts[b:e], a, i, None, tol, max_iter,
+                                    fk_err=torch.empty(e - b, dtype=torch.float64, device="cuda"))
+            return {"ang": a, "iters": i}
+        res["gather_check"] = gather_check(job, {"ang": dang, "iters": dit}, resolve)
     mx, sm, sum_iters, n_capped = _stats_over_ranks(job, st, res)
     if args.cold:
         res["cold"] = cold_steps(ctx, step)
@@ -500,13 +585,19 @@ def run_fk(job, args):
 
 
 def timed(ctx, step, args, world):
+    """W warm-up steps, one step timed per kernel, then K steps between barriers.
+    Every wait on the steps is ctx.sync() first (ik_ctx_sync): bounded by the
+    communicator's deadline at N > 1, so a stuck peer ends the run with
+    IK_E_RCCL rather than hanging it; torch.cuda.synchronize() then returns at once."""
     import torch
     for _ in range(args.warmup):
         step()
+    ctx.sync()
     torch.cuda.synchronize()
     # per-kernel HIP-event durations of one representative step
     ctx.set_timing(True)
     step()
+    ctx.sync()
     kernels = {}
     for name, ms in ctx.kernel_times():
         kernels[name] = kernels.get(name, 0.0) + ms
@@ -521,6 +612,7 @@ def timed(ctx, step, args, world):
     for _ in range(args.steps):
         step()
     ev1.record()
+    ctx.sync()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -546,9 +638,11 @@ def cold_steps(ctx, step, reps=3):
         e0.record()
         step()
         e1.record()
+        ctx.sync()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1))
     step()  # re-learn before anything else runs
+    ctx.sync()
     torch.cuda.synchronize()
     return {"ms": float(np.median(times)), "all_ms": times,
             "note": "work-order table reset before each call (ik_fabrik_reset_order): point "
@@ -776,6 +870,7 @@ def main():
         runners[f"ann_{om}"] = (lambda mm: lambda j, a: run_ann(j, a, mode=mm))(om)
     res = runners[args.method](job, args)
     outputs = {args.method: res["outputs"]}
+    checks = {args.method: res.get("gather_check")}
     secondary = {}
     if args.secondary and args.method != "fk":
         others = (["fabrik", "fabrik_tol1e-5"] + [f"ann_{om}" for om in other_modes] + ["fk"]
@@ -784,6 +879,7 @@ def main():
             others.remove("fabrik_tol1e-5")
         for other in others:
             r2 = runners[other](job, args)
+            checks[other] = r2.get("gather_check")
             secondary[other] = {"value": r2.get("total", total) / (r2["ms_per_step"] / 1e3),
                                 "unit": r2.get("unit", "IK solutions/s"),
                                 "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
@@ -791,7 +887,8 @@ def main():
                                 "kernels_ms": r2["kernels"],
                                 **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
                                                       "mean_iters", "n_capped", "end_to_end",
-                                                      "gather_chunks", "gather_ms", "cold")
+                                                      "gather_chunks", "gather_ms", "cold",
+                                                      "gather_check")
                                    if k in r2}}
             cref = _config_ref("fabrik" if other.startswith("fabrik") else other, total, world,
                                1e-5 if other == "fabrik_tol1e-5" else args.tol,
@@ -799,6 +896,7 @@ def main():
             if cref:
                 secondary[other]["baseline_config"] = cref
             outputs[other] = r2["outputs"]
+    gcheck, exit_code = gather_verdict(checks)
     value = res.get("total", total) / (res["ms_per_step"] / 1e3)
     line = {
         "metric": METRIC, "value": value, "unit": res.get("unit", "IK solutions/s"), "n_gpus": world,
@@ -823,6 +921,7 @@ def main():
                    if sc is not None else None,
                    "n_ranks_rccl": sc.info()[0] if sc is not None else None,
                    "gather_chunks": res.get("gather_chunks"),
+                   "gather_check": gcheck,
                    "tol": args.tol if args.method == "fabrik" else None,
                    "max_iter": args.max_iter if args.method == "fabrik" else None},
         "roofline": res["roofline"],
@@ -862,13 +961,17 @@ def main():
         sc.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
+        if exit_code:
+            print("bench.py: gathered rows differ from their plain re-solve "
+                  f"({json.dumps(gcheck)})", file=sys.stderr)
     if _dist_on():
         import torch.distributed as dist
         dist.destroy_process_group()
+    return exit_code
 
 
 if __name__ == "__main__":
     rc = maybe_launch()
     if rc is not None:
         sys.exit(rc)
-    main()
+    sys.exit(main())

@@ -197,6 +197,11 @@ int ik_host_free(void *p);
 /* After IK_F_ASYNC calls: wait for the stream and read the accumulated stats
  * of the last call. */
 int ik_stats_fetch(ik_ctx *ctx, ik_stats *stats);
+/* Wait for the context's last call.  With a communicator bound (ik_comm_init)
+ * the wait is bounded: it polls RCCL's async error and, past the deadline
+ * (ik_comm_set_timeout), aborts the communicator and returns IK_E_RCCL -- so an
+ * IK_F_ASYNC caller (e.g. a benchmark loop) never hangs on a dead peer. */
+int ik_ctx_sync(ik_ctx *ctx);
 
 /* ---- multi-GPU: RCCL over xGMI ------------------------------
  * The reference scales by competing consumers of one RabbitMQ queue
@@ -247,23 +252,42 @@ enum { IK_METHOD_ANN = 0, IK_METHOD_FABRIK = 1 };
 /* One rank creates the id and hands it to the others (any transport). */
 int ik_comm_unique_id(uint8_t *id /* IK_COMM_ID_BYTES */);
 /* Collective over the nranks processes: binds the context to an RCCL
- * communicator (one GPU per rank). */
+ * communicator (one GPU per rank).  The communicator is non-blocking
+ * (ncclCommInitRankConfig, blocking = 0): every host wait on it -- the
+ * rendezvous, group ends, a synchronous call's end, ik_ctx_sync,
+ * ik_stats_fetch -- polls ncclCommGetAsyncError against a deadline
+ * (IKHIP_RCCL_TIMEOUT_S, default 120 s; ik_comm_set_timeout) and on an error or
+ * timeout calls ncclCommAbort and returns IK_E_RCCL naming the rank and the
+ * wait.  An aborted communicator (also after any failure part-way through a
+ * sharded call) refuses later calls until ik_comm_destroy + ik_comm_init.  Its
+ * first act is one all-gather of a 64-byte record per rank that checks the
+ * ranks agree (numbering, IKHIP_GATHER_CHUNKS, library version). */
 int ik_comm_init(ik_ctx *ctx, int nranks, int rank, const uint8_t *id);
+/* The deadline of the communicator's waits in seconds (0: IKHIP_RCCL_TIMEOUT_S
+ * or 120).  Kept across ik_comm_init. */
+int ik_comm_set_timeout(ik_ctx *ctx, double seconds);
 /* TEST-ONLY: a communicator without RCCL, so that one GPU can run the sharded
  * path as rank `rank` of `nranks` (the placement of every part, the ragged
  * chunk's stage, the tail reduction).  Its all-gather writes byte o of rank
  * s's slot as ik_loopback_byte(s, o) for every s != rank, and copies this
  * rank's tail block into every rank's. */
 int ik_comm_init_loopback(ik_ctx *ctx, int nranks, int rank);
+/* TEST-ONLY: with on != 0 the loopback communicator's all-gathers wait for a
+ * peer that never comes (each block spins on a pinned flag, at most 30 s), so a
+ * test can drive the deadline path: the wait times out, the abort releases the
+ * flag, the GPU drains, the call returns IK_E_RCCL. */
+int ik_comm_loopback_stall(ik_ctx *ctx, int on);
 int ik_loopback_byte(int slot, int64_t offset);
 int ik_comm_destroy(ik_ctx *ctx);
 /* The communicator as the library holds it: ranks, this rank, and the chunk
  * count the last sharded call was planned with (ik_shard_plan_of's chunks; 0
  * before one), so a caller can find its own rows with ik_shard_part. */
 int ik_comm_info(ik_ctx *ctx, int *nranks, int *rank, int *last_chunks);
-/* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic: FABRIK
- * 2 when a rank's share is >= 512k rows, else 1; ANN 1 (its gather is ~1 % of
- * its solve).  Environment default: IKHIP_GATHER_CHUNKS. */
+/* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic (1: one
+ * in-place all-gather after the solve).  Every rank must use the same value:
+ * each call's tail carries its plan (n, chunks, method) and a rank whose plan
+ * differs from rank 0's fails the call with IK_E_RCCL.  Environment default:
+ * IKHIP_GATHER_CHUNKS (checked equal on every rank by ik_comm_init). */
 int ik_comm_set_chunks(ik_ctx *ctx, int chunks);
 /* Host-only helpers of the protocol (no device needed). */
 int ik_shard_plan_of(int64_t n, int nranks, int chunks, ik_shard_plan *out);

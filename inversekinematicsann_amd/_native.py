@@ -40,7 +40,8 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_comm_set_chunks", "ik_shard_plan_of", "ik_shard_part", "ik_shard_range",
                     "ik_tail_reduce", "ik_fkhist_bin", "ik_fkhist_upper", "ik_fk_err_quantile",
                     "ik_ann_solve_sharded", "ik_fabrik_solve_sharded", "ik_host_alloc",
-                    "ik_host_free")
+                    "ik_host_free", "ik_ctx_sync", "ik_comm_set_timeout",
+                    "ik_comm_loopback_stall")
 ANN_MODES = {"fp32": 0, "bf16x6": 1, "fp16x3": 2}
 
 
@@ -126,6 +127,9 @@ def load_library(path: str = LIB_PATH):
                                   ctypes.POINTER(ctypes.c_void_p), dp, dp, dp, dp]
         L.ik_ann_solve.argtypes = [vp, dp, i64, dp, dp, ctypes.c_int, st]
         L.ik_stats_fetch.argtypes = [vp, st]
+        L.ik_ctx_sync.argtypes = [vp]
+        L.ik_comm_set_timeout.argtypes = [vp, ctypes.c_double]
+        L.ik_comm_loopback_stall.argtypes = [vp, ctypes.c_int]
         L.ik_ctx_set_timing.argtypes = [vp, ctypes.c_int]
         L.ik_kernel_times.argtypes = [vp, ctypes.c_int, vp, vp, ctypes.c_int]
         L.ik_ctx_set_debug.argtypes = [vp, ctypes.c_int]
@@ -443,6 +447,20 @@ class Context:
     def comm_destroy(self):
         self._check(self.lib.ik_comm_destroy(self.handle))
 
+    def comm_set_timeout(self, seconds: float):
+        """Deadline of the communicator's host waits (0: IKHIP_RCCL_TIMEOUT_S or 120 s)."""
+        self._check(self.lib.ik_comm_set_timeout(self.handle, float(seconds)))
+
+    def comm_loopback_stall(self, on: bool = True):
+        """TEST-ONLY (ik_comm_loopback_stall): the loopback all-gathers wait for a
+        peer that never comes, until the deadline's abort releases them."""
+        self._check(self.lib.ik_comm_loopback_stall(self.handle, 1 if on else 0))
+
+    def sync(self):
+        """Wait for the last call (ik_ctx_sync): bounded by the communicator's
+        deadline when one is bound; raises NativeError(IK_E_RCCL) on abort."""
+        self._check(self.lib.ik_ctx_sync(self.handle))
+
     def comm_info(self):
         """(ranks of the library's communicator, this rank, chunks of the last sharded call)."""
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
@@ -468,7 +486,8 @@ class Context:
         p = _host(pts, np.float64, 3)
         n = p.shape[0]
         ang = np.empty((n, 4), np.float32)
-        err = np.empty(n, np.float64) if want_fk_err else None
+        # only this rank's rows of fk_err are written (ikhip.h): the rest stay NaN
+        err = np.full(n, np.nan) if want_fk_err else None
         flags = 0 if check_limits else IK_F_NO_LIMITS
         self._check(self.lib.ik_ann_solve_sharded(self.handle, _ptr(p), n, _ptr(ang), _ptr(err),
                                                   flags, ctypes.byref(s)))
@@ -481,7 +500,8 @@ class Context:
         n = p.shape[0]
         ang = np.empty((n, 4), np.float64)
         it = np.empty(n, np.int32)
-        err = np.empty(n, np.float64) if want_fk_err else None
+        # only this rank's rows of fk_err are written (ikhip.h): the rest stay NaN
+        err = np.full(n, np.nan) if want_fk_err else None
         flags = 0 if check_limits else IK_F_NO_LIMITS
         self._check(self.lib.ik_fabrik_solve_sharded(self.handle, _ptr(p), n, float(tol),
                                                      int(max_iter), _ptr(ang), _ptr(it),

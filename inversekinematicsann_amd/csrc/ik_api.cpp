@@ -209,6 +209,11 @@ int ik_ctx_create(int device, ik_ctx **out) {
 int ik_ctx_destroy(ik_ctx *c) {
   if (!c) return IK_OK;
   (void)hipSetDevice(c->device);
+  // the communicator first: a live one's last call is waited for with its
+  // deadline; an aborted one whose work has not drained leaves the context's
+  // device memory to the process's end rather than block on it
+  if (!comm_release(c)) return fail(IK_E_RCCL, "ik_ctx_destroy: aborted collective work has not "
+                                               "drained; the context is left to the process's end");
   (void)hipStreamSynchronize(c->stream);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->ann_buf) (void)hipFree(c->ann_buf);
@@ -217,7 +222,6 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->fab_ord) (void)hipFree(c->fab_ord);
   if (c->rconst) (void)hipFree(c->rconst);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
-  comm_release(c);
   pipe_release(c);
   if (c->call_done) (void)hipEventDestroy(c->call_done);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -326,6 +330,16 @@ int ik_debug_read(ik_ctx *c, uint64_t *out, int max) {
   if (hipMemcpy(out, c->dbg, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return -IK_E_HIP;
   return n;
+}
+
+int ik_ctx_sync(ik_ctx *c) {
+  if (!c) return fail(IK_E_BADARG, "ik_ctx_sync: NULL context");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  if (c->last_piped) return IK_OK;  // a chunked host pipeline returns complete
+  if (!c->call_done_set) return IK_OK;
+  // with a communicator the wait is bounded (its deadline and async errors)
+  return comm_wait(c, c->call_done, "the last call");
 }
 
 int ik_stats_fetch(ik_ctx *c, ik_stats *stats) {

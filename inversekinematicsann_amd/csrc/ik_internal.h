@@ -22,9 +22,20 @@ struct KTimer {
 };
 }  // namespace ikhip
 
-// One rank's tail block as gathered: the stats record, then its FK-error histogram.
+// What a rank planned its sharded call with; every rank's must agree (a rank
+// that planned another batch or chunk count gathered other rows).
+struct IkPlanHdr {
+  int64_t n;
+  int32_t chunks, method;
+  uint32_t magic, pad;
+};
+constexpr uint32_t kPlanMagic = 0x494b5348u;  // "IKSH"
+
+// One rank's tail block as gathered: the stats record, the plan, then its
+// FK-error histogram.
 struct IkTailBlock {
   ik_shard_tail t;
+  IkPlanHdr plan;
   uint32_t hist[IK_FKHIST_BINS];
 };
 
@@ -50,6 +61,19 @@ struct IkComm {
   hipEvent_t ev_solved[IK_MAX_GATHER_CHUNKS] = {};  // chunk k's rows written (solve stream)
   hipEvent_t ev_gs[IK_MAX_GATHER_CHUNKS] = {}, ev_ge[IK_MAX_GATHER_CHUNKS] = {};  // gather k
   hipEvent_t ev_done = nullptr;  // the call's last gather / copy on cs
+  // Bounded waits (ik_shard.hip comm_wait): every host wait on the collective
+  // polls the communicator's async error against this deadline and aborts the
+  // communicator when it passes, so a dead or stuck peer ends in IK_E_RCCL
+  // instead of a hang.  0 = IKHIP_RCCL_TIMEOUT_S, else 120 s.
+  double timeout_s = 0.0;
+  bool broken = false;   // aborted (deadline, async error, mid-call failure): calls refuse
+  std::string why;       // ... and why
+  hipEvent_t ev_end = nullptr;  // the last sharded call's end on its solve stream
+  bool ev_end_set = false;
+  // ik_comm_loopback_stall (test-only): the loopback all-gathers spin on this
+  // pinned flag until the deadline's abort sets it (or their own 30 s cap)
+  int *stall_flag = nullptr;
+  bool stall = false;
 };
 
 // The chunked host-pointer pipeline (ik_pipe.cpp): copy streams, per-chunk
@@ -145,6 +169,11 @@ int fabrik_host_pipeline(ik_ctx *c, const double *pts, int64_t n, double tol, in
 void pipe_release(ik_ctx *c);
 // The batch stats of the last sharded call, from the gathered tails (waits).
 int sharded_stats(ik_ctx *c, ik_stats *stats);
-void comm_release(ik_ctx *c);
+// Releases the communicator; false when aborted work has not drained (its
+// buffers are then left to the process's end).
+bool comm_release(ik_ctx *c);
+// Waits for `ev` with the communicator's deadline and async-error polling when
+// the context holds a live communicator (else a plain hipEventSynchronize).
+int comm_wait(ik_ctx *c, hipEvent_t ev, const char *what);
 
 }  // namespace ikapi

@@ -28,11 +28,15 @@
 #include <link.h>
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include "ik_internal.h"
 
@@ -47,23 +51,46 @@ typedef int (*GetUniqueIdFn)(void *id);
 struct IdBlob {
   char b[IK_COMM_ID_BYTES];
 };
+// ncclConfig_t as rccl.h (ncclConfig_v22700) lays it out.  RCCL copies
+// min(size, its own sizeof) bytes of it, so an older librccl (torch's 2.26)
+// reads the prefix it knows; NCCL_CONFIG_INITIALIZER's values, blocking = 0.
+struct NcclConfig {
+  size_t size = sizeof(NcclConfig);
+  unsigned int magic = 0xcafebeefu;
+  unsigned int version = 22707;  // NCCL_VERSION(2, 27, 7)
+  int blocking = 0;              // non-blocking: init and group ends return ncclInProgress
+  int cga_cluster_size = INT32_MIN, min_ctas = INT32_MIN, max_ctas = INT32_MIN;
+  const char *net_name = nullptr;
+  int split_share = INT32_MIN, traffic_class = INT32_MIN;
+  const char *comm_name = nullptr;
+  int collnet_enable = INT32_MIN, cta_policy = INT32_MIN, shrink_share = INT32_MIN,
+      nvls_ctas = INT32_MIN;
+};
 typedef int (*CommInitRankBlobFn)(void **comm, int nranks, IdBlob id, int rank);
-typedef int (*CommDestroyFn)(void *comm);
+typedef int (*CommInitRankConfigFn)(void **comm, int nranks, IdBlob id, int rank,
+                                    NcclConfig *config);
+typedef int (*CommFn)(void *comm);
+typedef int (*CommAsyncErrorFn)(void *comm, int *result);
 typedef int (*AllGatherFn)(const void *send, void *recv, size_t count, int dtype, void *comm,
                            hipStream_t stream);
 typedef int (*GroupFn)();
 typedef const char *(*GetErrorStringFn)(int);
-constexpr int kNcclUint8 = 1;  // ncclDataType_t ncclUint8
+constexpr int kNcclUint8 = 1;       // ncclDataType_t ncclUint8
+constexpr int kNcclInProgress = 7;  // ncclResult_t ncclInProgress
 
 struct Rccl {
   void *lib = nullptr;
   GetUniqueIdFn get_unique_id = nullptr;
   CommInitRankBlobFn comm_init_rank = nullptr;
-  CommDestroyFn comm_destroy = nullptr;
+  CommInitRankConfigFn comm_init_rank_config = nullptr;  // non-blocking init (may be absent)
+  CommFn comm_destroy = nullptr, comm_abort = nullptr;
+  CommAsyncErrorFn comm_async_error = nullptr;
   AllGatherFn all_gather = nullptr;
   GroupFn group_start = nullptr, group_end = nullptr;
   GetErrorStringFn error_string = nullptr;
   std::string where;
+  // the bounded-wait path needs all three; else the communicator is blocking
+  bool nonblocking() const { return comm_init_rank_config && comm_abort && comm_async_error; }
 };
 
 std::mutex g_rccl_mu;
@@ -115,7 +142,11 @@ int load_rccl(Rccl **out) {
     r.where = where;
     r.get_unique_id = reinterpret_cast<GetUniqueIdFn>(dlsym(h, "ncclGetUniqueId"));
     r.comm_init_rank = reinterpret_cast<CommInitRankBlobFn>(dlsym(h, "ncclCommInitRank"));
-    r.comm_destroy = reinterpret_cast<CommDestroyFn>(dlsym(h, "ncclCommDestroy"));
+    r.comm_init_rank_config =
+        reinterpret_cast<CommInitRankConfigFn>(dlsym(h, "ncclCommInitRankConfig"));
+    r.comm_destroy = reinterpret_cast<CommFn>(dlsym(h, "ncclCommDestroy"));
+    r.comm_abort = reinterpret_cast<CommFn>(dlsym(h, "ncclCommAbort"));
+    r.comm_async_error = reinterpret_cast<CommAsyncErrorFn>(dlsym(h, "ncclCommGetAsyncError"));
     r.all_gather = reinterpret_cast<AllGatherFn>(dlsym(h, "ncclAllGather"));
     r.group_start = reinterpret_cast<GroupFn>(dlsym(h, "ncclGroupStart"));
     r.group_end = reinterpret_cast<GroupFn>(dlsym(h, "ncclGroupEnd"));
@@ -133,6 +164,89 @@ int load_rccl(Rccl **out) {
 int rccl_fail(const Rccl *r, const char *what, int res) {
   const char *msg = (r && r->error_string) ? r->error_string(res) : "?";
   return fail(IK_E_RCCL, std::string(what) + ": " + msg + " (" + std::to_string(res) + ")");
+}
+
+// ---- bounded waits -----------------------------------------------------------
+using Clock = std::chrono::steady_clock;
+
+double since(Clock::time_point t0) {
+  return std::chrono::duration<double>(Clock::now() - t0).count();
+}
+
+// One poll's back-off: yield for the first ~2000 polls (a few ms), then sleep 50 us.
+void backoff(int &spins) {
+  if (++spins < 2000)
+    std::this_thread::yield();
+  else
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+}
+
+double comm_timeout(const IkComm &m) {
+  if (m.timeout_s > 0.0) return m.timeout_s;
+  static double env = -1.0;
+  if (env < 0.0) {
+    const char *e = std::getenv("IKHIP_RCCL_TIMEOUT_S");
+    const double v = (e && *e) ? std::atof(e) : 0.0;
+    env = v > 0.0 ? v : 120.0;
+  }
+  return env;
+}
+
+std::string rank_tag(const IkComm &m) {
+  return "rank " + std::to_string(m.rank) + " of " + std::to_string(m.nranks);
+}
+
+std::string secs_str(double s) {
+  char b[32];
+  std::snprintf(b, sizeof(b), "%.3g", s);
+  return b;
+}
+
+// A non-blocking communicator's pending operation (init, a group end, a lone
+// collective): poll its async state until it leaves ncclInProgress or the
+// deadline passes.  Returns the final ncclResult_t, or -1 on timeout.
+int rccl_settle(Rccl *r, void *comm, double timeout) {
+  if (!r->comm_async_error) return 0;
+  const Clock::time_point t0 = Clock::now();
+  int spins = 0;
+  for (;;) {
+    int st = 0;
+    const int q = r->comm_async_error(comm, &st);
+    if (q != 0) return q;
+    if (st != kNcclInProgress) return st;
+    if (since(t0) > timeout) return -1;
+    backoff(spins);
+  }
+}
+
+// Marks the communicator unusable and stops its collectives: ncclCommAbort (the
+// RCCL kernels poll its abort flag and exit), or for the loopback the stall
+// flag; then lets `drain` complete for up to 10 s.  Returns IK_E_RCCL(why).
+int comm_abort(ik_ctx *c, hipEvent_t drain, const std::string &why) {
+  IkComm &m = c->comm;
+  if (!m.broken) {
+    m.broken = true;
+    m.why = why;
+    if (m.loopback) {
+      if (m.stall_flag) __atomic_store_n(m.stall_flag, 1, __ATOMIC_SEQ_CST);
+    } else {
+      Rccl *r = nullptr;
+      if (load_rccl(&r) == IK_OK && r->comm_abort) (void)r->comm_abort(m.comm);
+    }
+  }
+  if (drain) {
+    const Clock::time_point t0 = Clock::now();
+    int spins = 0;
+    while (hipEventQuery(drain) == hipErrorNotReady && since(t0) < 10.0) backoff(spins);
+  }
+  return fail(IK_E_RCCL, why);
+}
+
+// Whether the communicator's streams hold no pending work (after an abort).
+bool comm_drained(const IkComm &m) {
+  if (m.cs && hipStreamQuery(m.cs) == hipErrorNotReady) return false;
+  if (m.ev_end_set && hipEventQuery(m.ev_end) == hipErrorNotReady) return false;
+  return true;
 }
 
 bool plan_args_ok(int64_t n, int nranks, int chunks) {
@@ -187,10 +301,13 @@ struct TailArgs {
   int K;
   int64_t base[IK_MAX_GATHER_CHUNKS];  // global row of each chunk's part's first row
   int64_t rows;
+  IkPlanHdr plan;  // what this rank planned the call with
 };
 
-__global__ void pack_tail_kernel(TailArgs a, ik_shard_tail *t) {
+__global__ void pack_tail_kernel(TailArgs a, IkTailBlock *blk) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  blk->plan = a.plan;
+  ik_shard_tail *t = &blk->t;
   ik_shard_tail o;
   o.first_oob = -1;
   o.first_err = -1;
@@ -229,9 +346,22 @@ __host__ __device__ inline uint8_t loopback_byte(int slot, uint64_t o) {
   return (uint8_t)(((uint32_t)slot * 29u + (uint32_t)o * 13u + (uint32_t)(o >> 7)) ^ 0xA5u);
 }
 
+// stall (ik_comm_loopback_stall, test-only): a pinned host flag; every block
+// first waits for it to turn non-zero -- a peer that never arrives -- or for
+// cap_ticks of the 100 MHz wall clock, so the grid always drains.
 __global__ __launch_bounds__(256) void loopback_gather_kernel(const uint8_t *send, uint8_t *recv,
                                                               uint64_t cnt, int g, int me,
-                                                              int replicate) {
+                                                              int replicate, const int *stall,
+                                                              long long cap_ticks) {
+  if (stall) {
+    if (threadIdx.x == 0) {
+      const long long t0 = wall_clock64();
+      while (__hip_atomic_load(stall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 &&
+             wall_clock64() - t0 < cap_ticks)
+        __builtin_amdgcn_s_sleep(127);
+    }
+    __syncthreads();
+  }
   const uint64_t tot = cnt * (uint64_t)g;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot;
        i += (uint64_t)gridDim.x * blockDim.x) {
@@ -245,22 +375,27 @@ __global__ __launch_bounds__(256) void loopback_gather_kernel(const uint8_t *sen
 
 namespace {
 
+int env_chunks() {
+  static int env = -1;
+  if (env < 0) {
+    const char *e = std::getenv("IKHIP_GATHER_CHUNKS");
+    env = (e && *e) ? std::atoi(e) : 0;
+  }
+  return env;
+}
+
 int auto_chunks(ik_ctx *c, int method, int64_t n) {
   const IkComm &m = c->comm;
   int C = m.chunks_req;
-  if (C <= 0) {
-    static int env = -1;
-    if (env < 0) {
-      const char *e = std::getenv("IKHIP_GATHER_CHUNKS");
-      env = (e && *e) ? std::atoi(e) : 0;
-    }
-    C = env;
-  }
-  // automatic: overlap only where the gather is comparable to the solve, and in
-  // two chunks: every FABRIK launch has a tail of its own (its last long points),
-  // so four 250k-point launches cost ~1.6x one 1M-point launch (0.15 ms each
-  // against 0.38 ms, profiles/r03/e2e) while two 500k-point ones cost ~1.15x
-  if (C <= 0) C = (method == IK_METHOD_FABRIK && m.nranks > 1 && n / m.nranks >= 524288) ? 2 : 1;
+  if (C <= 0) C = env_chunks();
+  // automatic: one chunk.  Chunked gathers under the next chunk's solve are
+  // opt-in (ik_comm_set_chunks / IKHIP_GATHER_CHUNKS, the same on every rank:
+  // ik_comm_init checks the environment's, every call's tail its plan) until a
+  // run of two or more real ranks has checked them bit for bit against a plain
+  // solve; the one-chunk pattern is one in-place all-gather.
+  (void)method;
+  (void)n;
+  if (C <= 0) C = 1;
   return C > IK_MAX_GATHER_CHUNKS ? IK_MAX_GATHER_CHUNKS : C;
 }
 
@@ -274,12 +409,17 @@ int ensure_comm_state(ik_ctx *c, size_t stage) {
       IK_HIP(hipEventCreate(&m.ev_ge[k]));
     }
     IK_HIP(hipEventCreateWithFlags(&m.ev_done, hipEventDisableTiming));
+    IK_HIP(hipEventCreateWithFlags(&m.ev_end, hipEventDisableTiming));
     IK_HIP(hipMalloc(&m.d_cstats, sizeof(DevStats) * IK_MAX_GATHER_CHUNKS));
     IK_HIP(hipMalloc(&m.tail_send, sizeof(IkTailBlock)));
   }
-  // the previous call's gathers finished before its solve stream did (it waited
-  // for ev_done), so syncing that stream frees every buffer below
-  if (stage > m.stage_bytes || m.tails_n < m.nranks) IK_HIP(hipStreamSynchronize(c->stream));
+  // the previous sharded call's gathers finished before its solve stream did
+  // (it waited for ev_done), so its end frees every buffer below; waited for
+  // with the deadline (a stuck peer aborts the communicator, not this thread)
+  if ((stage > m.stage_bytes || m.tails_n < m.nranks) && m.ev_end_set) {
+    const int rc = comm_wait(c, m.ev_end, "the previous sharded call");
+    if (rc) return rc;
+  }
   if (stage > m.stage_bytes) {
     if (m.stage) IK_HIP(hipFree(m.stage));
     m.stage = nullptr;
@@ -325,30 +465,47 @@ struct PartJob {
 // chunk on the comm stream; the tail block with the last chunk; the ragged
 // chunk's rows out of the stage; the solve stream waits for the gathers.
 template <class Solve>
-int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nreg,
-                double *fk_err_dev, Solve solve) {
+int sharded_enqueue(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nreg,
+                    double *fk_err_dev, Solve solve, int *gathers) {
   IkComm &m = c->comm;
   Rccl *r = nullptr;
   int rc = m.loopback ? IK_OK : load_rccl(&r);
   if (rc) return rc;
   const int g = m.nranks, me = m.rank, C = P.chunks;
-  // one all-gather of cnt bytes per rank on the comm stream (inside a group)
+  const double T = comm_timeout(m);
+  long long cap_ticks = 0;
+  if (m.loopback && m.stall) {
+    int khz = 0;
+    IK_HIP(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    cap_ticks = (long long)(khz > 0 ? khz : 100000) * 1000 * 30;  // 30 s
+  }
+  // one all-gather of cnt bytes per rank on the comm stream (inside a group);
+  // a non-blocking communicator may answer ncclInProgress (settled at the group end)
   auto gather = [&](const void *send, void *recv, size_t cnt, bool replicate) -> int {
+    ++*gathers;
     if (m.loopback) {
       const uint64_t tot = (uint64_t)cnt * g, blocks = (tot + 255) / 256;
       if (tot)
         hipLaunchKernelGGL(loopback_gather_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)),
                            dim3(256), 0, m.cs, static_cast<const uint8_t *>(send),
-                           static_cast<uint8_t *>(recv), (uint64_t)cnt, g, me, replicate ? 1 : 0);
+                           static_cast<uint8_t *>(recv), (uint64_t)cnt, g, me, replicate ? 1 : 0,
+                           m.stall ? m.stall_flag : nullptr, cap_ticks);
       IK_HIP(hipGetLastError());
       return IK_OK;
     }
     const int res = r->all_gather(send, recv, cnt, kNcclUint8, m.comm, m.cs);
-    return res ? rccl_fail(r, "ncclAllGather", res) : IK_OK;
+    return (res && res != kNcclInProgress) ? rccl_fail(r, "ncclAllGather", res) : IK_OK;
   };
+  // the group end of a non-blocking communicator enqueues asynchronously: wait
+  // (bounded) until the kernels are on the comm stream before recording its events
   auto group = [&](bool start) -> int {
     if (m.loopback) return IK_OK;
-    const int res = start ? r->group_start() : r->group_end();
+    int res = start ? r->group_start() : r->group_end();
+    if (!start && res == kNcclInProgress) {
+      res = rccl_settle(r, m.comm, T);
+      if (res < 0)
+        return fail(IK_E_RCCL, "ncclGroupEnd did not settle within " + secs_str(T) + " s");
+    }
     return res ? rccl_fail(r, start ? "ncclGroupStart" : "ncclGroupEnd", res) : IK_OK;
   };
   const int64_t S = P.part_rows;
@@ -360,6 +517,10 @@ int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nr
   std::memset(&ta, 0, sizeof(ta));
   ta.S = m.d_cstats;
   ta.K = C;
+  ta.plan.n = P.n;
+  ta.plan.chunks = C;
+  ta.plan.method = method;
+  ta.plan.magic = kPlanMagic;
   for (int k = 0; k < C; ++k) {
     int64_t b, e;
     part_of(P, me, k, &b, &e);
@@ -390,7 +551,7 @@ int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nr
     }
     const bool last = k == C - 1;
     if (last) {
-      hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, &m.tail_send->t);
+      hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, m.tail_send);
     }
     IK_HIP(hipGetLastError());
     IK_HIP(hipEventRecord(m.ev_solved[k], c->stream));
@@ -420,12 +581,18 @@ int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nr
   if (C == 0) {  // an empty batch: every rank still exchanges its (empty) tail
     launch_reset_stats(m.d_cstats, c->stream);
     ta.K = 1;
-    hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, &m.tail_send->t);
+    hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, m.tail_send);
     IK_HIP(hipGetLastError());
     IK_HIP(hipEventRecord(m.ev_solved[0], c->stream));
     IK_HIP(hipStreamWaitEvent(m.cs, m.ev_solved[0], 0));
     IK_HIP(hipEventRecord(m.ev_gs[0], m.cs));
-    if ((rc = gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), true))) return rc;
+    if ((rc = group(true))) return rc;
+    rc = gather(m.tail_send, m.tail_recv, sizeof(IkTailBlock), true);
+    if (rc) {
+      (void)group(false);
+      return rc;
+    }
+    if ((rc = group(false))) return rc;
     IK_HIP(hipEventRecord(m.ev_ge[0], m.cs));
     m.last_chunks = 1;
   }
@@ -435,23 +602,98 @@ int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nr
   IK_HIP(hipStreamWaitEvent(c->stream, m.ev_done, 0));
   IK_HIP(hipMemcpyAsync(m.h_tails, m.tail_recv, sizeof(IkTailBlock) * (size_t)g,
                         hipMemcpyDeviceToHost, c->stream));
+  IK_HIP(hipEventRecord(m.ev_end, c->stream));
+  m.ev_end_set = true;
   c->last_sharded = true;
   c->last_n = P.n;
-  (void)method;
   return IK_OK;
+}
+
+// sharded_enqueue, and on a failure part-way (a solve launch, a collective call,
+// the group end's deadline) the solve stream still ends after whatever reached
+// the comm stream, and the communicator is aborted: this rank's sequence of
+// collectives no longer matches its peers', so no later call may use it
+// (ADVICE r03).
+template <class Solve>
+int sharded_run(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, int nreg,
+                double *fk_err_dev, Solve solve) {
+  IkComm &m = c->comm;
+  if (m.broken) return fail(IK_E_RCCL, "communicator aborted earlier (" + m.why +
+                                           "); ik_comm_destroy and ik_comm_init again");
+  int gathers = 0;
+  const int rc = sharded_enqueue(c, method, P, R, nreg, fk_err_dev, solve, &gathers);
+  if (rc == IK_OK) return IK_OK;
+  const std::string msg = ik_last_error();
+  if (hipEventRecord(m.ev_done, m.cs) == hipSuccess)
+    (void)hipStreamWaitEvent(c->stream, m.ev_done, 0);
+  c->last_sharded = false;
+  return comm_abort(c, m.ev_done, rank_tag(m) + ": sharded call failed after " +
+                                      std::to_string(gathers) + " all-gather(s) (" + msg +
+                                      "); communicator aborted");
 }
 
 }  // namespace
 
 namespace ikapi {
 
-int sharded_stats(ik_ctx *c, ik_stats *stats) {
-  IK_HIP(hipStreamSynchronize(c->stream));
-  if (!stats) return IK_OK;
+int comm_wait(ik_ctx *c, hipEvent_t ev, const char *what) {
   IkComm &m = c->comm;
+  if (!m.comm) {
+    IK_HIP(hipEventSynchronize(ev));
+    return IK_OK;
+  }
+  if (m.broken)  // already aborted: at most a bounded drain, then the old reason
+    return comm_abort(c, ev, "communicator aborted earlier (" + m.why + ")");
+  Rccl *r = nullptr;
+  if (!m.loopback && load_rccl(&r) != IK_OK) r = nullptr;
+  const double T = comm_timeout(m);
+  const Clock::time_point t0 = Clock::now();
+  int spins = 0;
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return IK_OK;
+    if (e != hipErrorNotReady)
+      return fail(IK_E_HIP, std::string("waiting for ") + what + ": " + hipGetErrorString(e));
+    if (r && r->comm_async_error) {
+      int st = 0;
+      if (r->comm_async_error(m.comm, &st) == 0 && st != 0 && st != kNcclInProgress) {
+        const char *msg = r->error_string ? r->error_string(st) : "?";
+        return comm_abort(c, ev, rank_tag(m) + ": " + what + ": RCCL async error " + msg + " (" +
+                                     std::to_string(st) + "); communicator aborted");
+      }
+    }
+    if (since(t0) > T)
+      return comm_abort(c, ev, rank_tag(m) + ": " + what + " did not complete within " +
+                                   secs_str(T) +
+                                   " s (IKHIP_RCCL_TIMEOUT_S / ik_comm_set_timeout): a peer "
+                                   "rank stopped or is in another collective; communicator "
+                                   "aborted");
+    backoff(spins);
+  }
+}
+
+int sharded_stats(ik_ctx *c, ik_stats *stats) {
+  IkComm &m = c->comm;
+  int rc = comm_wait(c, m.ev_end, "the sharded call");
+  if (rc) return rc;
+  // every rank planned the same call (same batch size, chunk count, method):
+  // else the rows it gathered belong to another plan
+  const IkPlanHdr &h0 = m.h_tails[0].plan;
+  for (int r = 0; r < m.nranks; ++r) {
+    const IkPlanHdr &h = m.h_tails[r].plan;
+    if (h.magic != kPlanMagic || h.n != h0.n || h.chunks != h0.chunks || h.method != h0.method)
+      return comm_abort(
+          c, nullptr,
+          rank_tag(m) + ": rank " + std::to_string(r) + " planned (n " + std::to_string(h.n) +
+              ", chunks " + std::to_string(h.chunks) + ", method " + std::to_string(h.method) +
+              ") but rank 0 (n " + std::to_string(h0.n) + ", chunks " +
+              std::to_string(h0.chunks) + ", method " + std::to_string(h0.method) +
+              "): every rank must pass the same batch and chunk setting; communicator aborted");
+  }
+  if (!stats) return IK_OK;
   ik_shard_tail t[1024];
   for (int r = 0; r < m.nranks; ++r) t[r] = m.h_tails[r].t;
-  int rc = ik_tail_reduce(t, m.nranks, stats);
+  rc = ik_tail_reduce(t, m.nranks, stats);
   if (rc) return rc;
   float tot = 0.0f;
   for (int k = 0; k < m.last_chunks; ++k) {
@@ -462,10 +704,23 @@ int sharded_stats(ik_ctx *c, ik_stats *stats) {
   return IK_OK;
 }
 
-void comm_release(ik_ctx *c) {
+bool comm_release(ik_ctx *c) {
   IkComm &m = c->comm;
+  // a live communicator's last call first ends, or is aborted at the deadline
+  if (m.comm && !m.broken && m.ev_end_set) (void)comm_wait(c, m.ev_end, "the last sharded call");
+  if (m.broken && !comm_drained(m)) {
+    // aborted work still queued: freeing its buffers would block on it, so
+    // they are left to the process's end (the communicator is unusable anyway)
+    const int keep_chunks = m.chunks_req;
+    const double keep_t = m.timeout_s;
+    m = IkComm();
+    m.chunks_req = keep_chunks;
+    m.timeout_s = keep_t;
+    c->last_sharded = false;
+    return false;
+  }
   if (m.cs) (void)hipStreamSynchronize(m.cs);
-  if (m.comm && !m.loopback) {
+  if (m.comm && !m.loopback && !m.broken) {  // (ncclCommAbort already freed an aborted one)
     Rccl *r = nullptr;
     if (load_rccl(&r) == IK_OK) (void)r->comm_destroy(m.comm);
   }
@@ -474,20 +729,87 @@ void comm_release(ik_ctx *c) {
   if (m.tail_recv) (void)hipFree(m.tail_recv);
   if (m.h_tails) (void)hipHostFree(m.h_tails);
   if (m.d_cstats) (void)hipFree(m.d_cstats);
+  if (m.stall_flag) (void)hipHostFree(m.stall_flag);
   for (int k = 0; k < IK_MAX_GATHER_CHUNKS; ++k) {
     if (m.ev_solved[k]) (void)hipEventDestroy(m.ev_solved[k]);
     if (m.ev_gs[k]) (void)hipEventDestroy(m.ev_gs[k]);
     if (m.ev_ge[k]) (void)hipEventDestroy(m.ev_ge[k]);
   }
   if (m.ev_done) (void)hipEventDestroy(m.ev_done);
+  if (m.ev_end) (void)hipEventDestroy(m.ev_end);
   if (m.cs) (void)hipStreamDestroy(m.cs);
   const int keep_chunks = m.chunks_req;
+  const double keep_t = m.timeout_s;
   m = IkComm();
   m.chunks_req = keep_chunks;
+  m.timeout_s = keep_t;
   c->last_sharded = false;
+  return true;
 }
 
 }  // namespace ikapi
+
+namespace {
+
+// The first collective of a new communicator: one all-gather of a 64-byte
+// record per rank, waited for with the deadline.  It checks the communicator
+// end to end before any solve relies on it, and that the ranks agree on what
+// their plans depend on (rank numbering, size, IKHIP_GATHER_CHUNKS, library).
+struct Hello {
+  uint32_t magic;
+  int32_t rank, nranks, env_chunks;
+  char version[48];
+};
+static_assert(sizeof(Hello) == 64, "Hello is one 64-byte slot");
+
+int comm_hello(ik_ctx *c, Rccl *r) {
+  IkComm &m = c->comm;
+  const int g = m.nranks;
+  int rc = ensure_comm_state(c, sizeof(Hello) * (size_t)g);
+  if (rc) return rc;
+  char *dev = static_cast<char *>(m.stage);
+  Hello *h = reinterpret_cast<Hello *>(m.h_tails);  // pinned, >= g slots of 64 B
+  Hello me;
+  std::memset(&me, 0, sizeof(me));
+  me.magic = kPlanMagic;
+  me.rank = m.rank;
+  me.nranks = g;
+  me.env_chunks = env_chunks();
+  std::snprintf(me.version, sizeof(me.version), "%s", ik_version());
+  h[m.rank] = me;
+  IK_HIP(hipMemcpyAsync(dev + (size_t)m.rank * sizeof(Hello), &h[m.rank], sizeof(Hello),
+                        hipMemcpyHostToDevice, m.cs));
+  int res = r->all_gather(dev + (size_t)m.rank * sizeof(Hello), dev, sizeof(Hello), kNcclUint8,
+                          m.comm, m.cs);
+  if (res == kNcclInProgress) res = rccl_settle(r, m.comm, comm_timeout(m));
+  if (res < 0) return comm_abort(c, nullptr, rank_tag(m) + ": the first all-gather did not settle");
+  if (res) {
+    rccl_fail(r, "ncclAllGather (first)", res);
+    return comm_abort(c, nullptr, rank_tag(m) + ": " + ik_last_error());
+  }
+  IK_HIP(hipMemcpyAsync(h, dev, sizeof(Hello) * (size_t)g, hipMemcpyDeviceToHost, m.cs));
+  IK_HIP(hipEventRecord(m.ev_end, m.cs));
+  m.ev_end_set = true;
+  if ((rc = comm_wait(c, m.ev_end, "the communicator's first all-gather"))) return rc;
+  for (int q = 0; q < g; ++q) {
+    const Hello &o = h[q];
+    std::string bad;
+    if (o.magic != kPlanMagic || o.rank != q || o.nranks != g)
+      bad = "slot " + std::to_string(q) + " holds rank " + std::to_string(o.rank) + " of " +
+            std::to_string(o.nranks);
+    else if (o.env_chunks != me.env_chunks)
+      bad = "rank " + std::to_string(q) + " has IKHIP_GATHER_CHUNKS " +
+            std::to_string(o.env_chunks) + ", this rank " + std::to_string(me.env_chunks);
+    else if (std::strncmp(o.version, me.version, sizeof(me.version)) != 0)
+      bad = "rank " + std::to_string(q) + " runs " + std::string(o.version, strnlen(o.version, 47));
+    if (!bad.empty())
+      return comm_abort(c, nullptr, rank_tag(m) + ": ranks disagree: " + bad +
+                                        "; communicator aborted");
+  }
+  return IK_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -510,17 +832,37 @@ int ik_comm_init(ik_ctx *c, int nranks, int rank, const uint8_t *id) {
   if (rc) return rc;
   Rccl *r = nullptr;
   if ((rc = load_rccl(&r))) return rc;
+  if (!comm_release(c)) return fail(IK_E_RCCL, "ik_comm_init: the aborted communicator's work "
+                                               "has not drained");
   (void)hipStreamSynchronize(c->stream);
-  comm_release(c);
   IdBlob b;
   std::memcpy(b.b, id, IK_COMM_ID_BYTES);
   void *comm = nullptr;
-  const int res = r->comm_init_rank(&comm, nranks, b, rank);
-  if (res != 0) return rccl_fail(r, "ncclCommInitRank", res);
-  c->comm.comm = comm;
   c->comm.nranks = nranks;
   c->comm.rank = rank;
-  return IK_OK;
+  const double T = comm_timeout(c->comm);
+  if (r->nonblocking()) {
+    // non-blocking: ncclCommInitRankConfig returns at once and the rendezvous
+    // with the other ranks is polled against the deadline
+    NcclConfig cfg;
+    int res = r->comm_init_rank_config(&comm, nranks, b, rank, &cfg);
+    if (res != 0 && res != kNcclInProgress) return rccl_fail(r, "ncclCommInitRankConfig", res);
+    res = rccl_settle(r, comm, T);
+    if (res != 0) {
+      if (comm) (void)r->comm_abort(comm);
+      if (res < 0)
+        return fail(IK_E_RCCL, rank_tag(c->comm) + ": ncclCommInitRankConfig did not complete "
+                                                   "within " + secs_str(T) +
+                                   " s (IKHIP_RCCL_TIMEOUT_S): a rank missing or another "
+                                   "unique id?");
+      return rccl_fail(r, "ncclCommInitRankConfig", res);
+    }
+  } else {  // an RCCL without the non-blocking API: a blocking init
+    const int res = r->comm_init_rank(&comm, nranks, b, rank);
+    if (res != 0) return rccl_fail(r, "ncclCommInitRank", res);
+  }
+  c->comm.comm = comm;
+  return comm_hello(c, r);
 }
 
 int ik_comm_init_loopback(ik_ctx *c, int nranks, int rank) {
@@ -528,12 +870,31 @@ int ik_comm_init_loopback(ik_ctx *c, int nranks, int rank) {
     return fail(IK_E_BADARG, "ik_comm_init_loopback: bad args");
   int rc = set_dev(c);
   if (rc) return rc;
+  if (!comm_release(c)) return fail(IK_E_RCCL, "ik_comm_init_loopback: the aborted "
+                                               "communicator's work has not drained");
   (void)hipStreamSynchronize(c->stream);
-  comm_release(c);
   c->comm.comm = &c->comm;  // a sentinel: never passed to RCCL
   c->comm.loopback = true;
   c->comm.nranks = nranks;
   c->comm.rank = rank;
+  return IK_OK;
+}
+
+int ik_comm_loopback_stall(ik_ctx *c, int on) {
+  if (!c || !c->comm.comm || !c->comm.loopback)
+    return fail(IK_E_BADARG, "ik_comm_loopback_stall: needs a loopback communicator");
+  IkComm &m = c->comm;
+  if (!m.stall_flag)
+    IK_HIP(hipHostMalloc(reinterpret_cast<void **>(&m.stall_flag), sizeof(int),
+                         hipHostMallocCoherent | hipHostMallocMapped));
+  __atomic_store_n(m.stall_flag, 0, __ATOMIC_SEQ_CST);
+  m.stall = on != 0;
+  return IK_OK;
+}
+
+int ik_comm_set_timeout(ik_ctx *c, double seconds) {
+  if (!c || !(seconds >= 0.0)) return fail(IK_E_BADARG, "ik_comm_set_timeout: bad args");
+  c->comm.timeout_s = seconds;
   return IK_OK;
 }
 
@@ -543,8 +904,10 @@ int ik_comm_destroy(ik_ctx *c) {
   if (!c) return fail(IK_E_BADARG, "ik_comm_destroy: NULL context");
   int rc = set_dev(c);
   if (rc) return rc;
+  if (!comm_release(c))
+    return fail(IK_E_RCCL, "ik_comm_destroy: the aborted communicator's work has not drained "
+                           "(its buffers are left to the process's end)");
   (void)hipStreamSynchronize(c->stream);
-  comm_release(c);
   return IK_OK;
 }
 
@@ -624,7 +987,7 @@ int ik_fk_err_quantile(ik_ctx *c, double q, double *out) {
     return fail(IK_E_BADARG, "ik_fk_err_quantile: the last call was not a sharded solve with fk_err");
   int rc = set_dev(c);
   if (rc) return rc;
-  IK_HIP(hipStreamSynchronize(c->last_stream ? c->last_stream : c->stream));
+  if ((rc = comm_wait(c, c->comm.ev_end, "the last sharded call"))) return rc;
   const IkComm &m = c->comm;
   uint64_t tot = 0;
   for (int r = 0; r < m.nranks; ++r)
@@ -722,6 +1085,9 @@ int ik_ann_solve_sharded(ik_ctx *c, const double *pts, int64_t n, float *ang, do
   const bool dev = flags & IK_F_DEVICE;
   const int g = c->comm.nranks;
   ik_shard_plan P;
+  if (c->comm.broken)
+    return fail(IK_E_RCCL, "ik_ann_solve_sharded: communicator aborted earlier (" +
+                               c->comm.why + ")");
   c->comm.last_req = auto_chunks(c, IK_METHOD_ANN, n);
   make_plan(n, g, c->comm.last_req, &P);
   const size_t stage = Stage::up((size_t)P.part_rows * g * 16);
@@ -766,6 +1132,9 @@ int ik_fabrik_solve_sharded(ik_ctx *c, const double *pts, int64_t n, double tol,
   const bool dev = flags & IK_F_DEVICE;
   const int g = c->comm.nranks;
   ik_shard_plan P;
+  if (c->comm.broken)
+    return fail(IK_E_RCCL, "ik_fabrik_solve_sharded: communicator aborted earlier (" +
+                               c->comm.why + ")");
   c->comm.last_req = auto_chunks(c, IK_METHOD_FABRIK, n);
   make_plan(n, g, c->comm.last_req, &P);
   const int nreg = iters ? 2 : 1;

@@ -84,3 +84,73 @@ def test_rank_count_mismatch_exits_nonzero():
                        env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 2 and p.stdout == ""
     assert "--gpus 8 but 1 rank" in p.stderr
+
+
+def test_gather_check_compare_rows_bitwise():
+    """compare_rows: bit-for-bit, row granular (a NaN equals itself by bits; -0.0
+    differs from 0.0), over every output of the check."""
+    import bench
+    a = np.arange(40, dtype=np.float64).reshape(10, 4)
+    it = np.arange(10, dtype=np.int32)
+    assert bench.compare_rows({"ang": a, "iters": it}, {"ang": a.copy(), "iters": it.copy()}) == \
+        (10, 0)
+    b = a.copy()
+    b[3, 2] = np.nextafter(b[3, 2], np.inf)  # one ulp in one row
+    b[7, 0] = -0.0 if a[7, 0] == 0.0 else -a[7, 0]
+    assert bench.compare_rows({"ang": a}, {"ang": b}) == (10, 2)
+    n = a.copy()
+    n[0, 0] = np.nan
+    assert bench.compare_rows({"ang": n}, {"ang": n.copy()}) == (10, 0)
+    it2 = it.copy()
+    it2[9] += 1
+    assert bench.compare_rows({"ang": a, "iters": it}, {"ang": a, "iters": it2}) == (10, 1)
+
+
+def test_gather_verdict_exits_nonzero_on_mismatch():
+    """a line whose gathered rows differ from their re-solve
+    carries bit_exact false and the bench exits 3; no check (N = 1) is None / 0."""
+    import bench
+    assert bench.gather_verdict({"ann": None}) == (None, 0)
+    ok = {"rows": 100, "mismatched_rows": 0, "bit_exact": True}
+    bad = {"rows": 50, "mismatched_rows": 2, "bit_exact": False}
+    g, rc = bench.gather_verdict({"ann": ok, "fabrik": ok})
+    assert rc == 0 and g["bit_exact"] and g["rows"] == 200
+    g, rc = bench.gather_verdict({"ann": ok, "fabrik": bad})
+    assert rc == 3 and not g["bit_exact"] and g["rows"] == 150
+
+
+def test_gather_check_parts_of_the_next_rank():
+    """The rows a rank re-solves: rank (r+1) % N's first and last parts in the
+    library's plan (chunks from ik_comm_info), and the check over them."""
+    import bench
+    from inversekinematicsann_amd import dist as D
+
+    class _SC:
+        def __init__(self, rank, chunks):
+            self.rank, self._c = rank, chunks
+
+        def info(self):
+            return (4, self.rank, self._c)
+
+    class _Job:
+        world, total = 4, 1003
+
+        def __init__(self, rank, chunks):
+            self.sc = _SC(rank, chunks)
+
+    assert bench._check_parts(_Job(0, 1)) == [D.part_bounds(1003, 4, 1, 1, 0)]
+    assert bench._check_parts(_Job(3, 1)) == [D.part_bounds(1003, 4, 1, 0, 0)]
+    parts = bench._check_parts(_Job(1, 3))
+    assert parts == [D.part_bounds(1003, 4, 3, 2, 0), D.part_bounds(1003, 4, 3, 2, 2)]
+    # the check over those parts: a gathered array equal to the re-solve passes,
+    # one corrupted row of the next rank's last part fails (world 1 here: no
+    # torch.distributed, the sums are the rank's own)
+    full = np.arange(1003 * 4, dtype=np.float32).reshape(1003, 4)
+    job = _Job(1, 3)
+    job.world = 4
+    res = bench.gather_check(job, {"ang": full}, lambda b, e: {"ang": full[b:e].copy()})
+    assert res["bit_exact"] and res["rows"] == sum(e - b for b, e in parts)
+    bad = full.copy()
+    bad[parts[-1][1] - 1, 3] += 1
+    res = bench.gather_check(job, {"ang": bad}, lambda b, e: {"ang": full[b:e].copy()})
+    assert not res["bit_exact"] and res["mismatched_rows"] == 1

@@ -284,3 +284,68 @@ def test_sharded_placement_at_2_and_3_ranks_loopback():
             assert abs(tot - ref["sum_fk_err"]) <= 1e-9 * max(1.0, ref["sum_fk_err"])
         if n == 5000:
             assert f_st["first_oob"] == 3400 and f_st["first_err"] == 4990
+
+
+def _stall_worker(q):
+    """the deadline path, driven on one GPU.  A loopback
+    communicator whose all-gathers wait for a peer that never comes
+    (ik_comm_loopback_stall): the synchronous sharded call returns IK_E_RCCL
+    naming the rank and the wait within the deadline, the abort releases the
+    stalled gather so the GPU drains, the communicator refuses later calls, and
+    after ik_comm_destroy + a new communicator the same context solves again
+    (bit-exact against a plain solve).  The same for an IK_F_ASYNC call ended by
+    ik_ctx_sync."""
+    import time
+    import torch
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd import dist as D
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    try:
+        out = {}
+        ctx = _native.Context(0)
+        pts = random_dist(4000, seed=9)
+        r_ang, r_it, _, _ = ctx.fabrik_solve(pts, 1e-3, 100)
+        for mode in ("sync", "async"):
+            sc = D.ShardedContext.loopback(ctx, 2, 0)
+            ctx.comm_set_timeout(2.0)
+            ctx.comm_loopback_stall(True)
+            t0 = time.perf_counter()
+            try:
+                if mode == "sync":
+                    sc.fabrik(pts, 1e-3, 100)
+                else:
+                    dpts = torch.from_numpy(pts).cuda()
+                    dang = torch.empty((4000, 4), dtype=torch.float64, device="cuda")
+                    sc.fabrik_device(dpts, dang, None, None, 1e-3, 100,
+                                     flags=_native.IK_F_DEVICE | _native.IK_F_ASYNC)
+                    ctx.sync()
+                out[mode] = ("no error", 0.0, "")
+            except _native.NativeError as e:
+                out[mode] = (e.code, time.perf_counter() - t0, str(e))
+            torch.cuda.synchronize()  # the abort released the stalled gather
+            try:
+                sc.fabrik(pts[:10], 1e-3, 100)
+                out[mode + "_refused"] = False
+            except _native.NativeError as e:
+                out[mode + "_refused"] = e.code == _native.IK_E_RCCL and "aborted" in str(e)
+            sc.close()
+            # a new communicator on the same context works again
+            sc = D.ShardedContext.loopback(ctx, 1, 0)
+            ang, it, _, _ = sc.fabrik(pts, 1e-3, 100)
+            out[mode + "_after"] = bool(np.array_equal(ang, r_ang) and np.array_equal(it, r_it))
+            sc.close()
+        q.put(out)
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put(repr(e) + traceback.format_exc())
+
+
+def test_stalled_gather_times_out_with_rccl_error():
+    from inversekinematicsann_amd import _native
+    res = _spawn(_stall_worker, timeout=120)
+    for mode in ("sync", "async"):
+        code, secs, msg = res[mode]
+        assert code == _native.IK_E_RCCL, (mode, res[mode])
+        assert 1.9 <= secs <= 15.0, (mode, secs)
+        assert "rank 0 of 2" in msg and "did not complete within 2 s" in msg, msg
+        assert res[mode + "_refused"] and res[mode + "_after"], (mode, res)
