@@ -224,6 +224,22 @@ def profile_fields(path, kernel):
     return out
 
 
+def roofline_fracs(work, kernel_ms, peak, prof):
+    """The roofline's achieved rate both ways: from this run's
+    HIP-event kernel time and from the committed rocprof window average of the
+    same kernel (`prof`: profile_fields); `frac` / `achieved` headline the
+    LOWER of the two.  work: algorithmic flop (or bytes) per launch."""
+    ev = work / (kernel_ms / 1e3) if kernel_ms else None
+    rp = prof.get("rocprof_avg_ms")
+    rq = work / (rp / 1e3) if rp else None
+    cands = [x for x in (ev, rq) if x]
+    head = min(cands) if cands else None
+    return {"achieved_events": ev, "frac_events": ev / peak if ev else None,
+            "achieved_rocprof": rq, "frac_rocprof": rq / peak if rq else None,
+            "headline": None if head is None else ("rocprof" if head == rq else "events"),
+            "_head": head}
+
+
 def load_pipe(path, kernel):
     """Pipe occupancy of `kernel` from the committed PMC diagnosis pass
     (tools/pmc_diag.sh -> tools/pmc_summary.py): MFMA busy, VALU active and
@@ -442,19 +458,23 @@ def run_ann(job, args, mode="fp32"):
     kname = "ann_fused_kernel" if mode == "fp32" else f"ann_fused_kernel_{mode}"
     k = res["kernels"].get(kname)
     n = job.n_local
-    achieved = flop_pt * n / (k / 1e3) if k else None
     # split modes: k bf16 / fp16 MFMA products per fp32 product, so the
     # fp32-equivalent matrix peak is the 16-bit peak / k (the input and output
     # layers stay fp32)
     peak = (FP32_MFMA_PEAK if mode == "fp32" else
             (BF16_MFMA_PEAK if mode == "bf16x6" else FP16_MFMA_PEAK) / SPLIT_PRODUCTS[mode])
     traffic = load_traffic(args.traffic_file, kname)
+    prof = profile_fields(args.traffic_file, kname)
+    fr = roofline_fracs(flop_pt * n, k, peak, prof)
+    achieved = fr.pop("_head")
     res["roofline"] = {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
                        "peak": peak / 1e12, "unit": "TFLOP/s",
                        "frac": achieved / peak if achieved else None,
+                       "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
+                       "frac_headline": fr["headline"],
                        "traffic": traffic, "kernel": kname,
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
-                       "points_per_launch": n, **profile_fields(args.traffic_file, kname)}
+                       "points_per_launch": n, **prof}
     diag = "ann_diag_summary.json" if mode == "fp32" else f"ann_{mode}_diag_summary.json"
     res["roofline"]["pipes"] = load_pipe(os.path.join(args.pmc_dir, diag), kname)
     if mode == "fp32":
@@ -485,14 +505,29 @@ def run_fabrik(job, args, tol=None, max_iter=None):
 
     # the --verbose FK round trip (cli.py:54-72) in the same launch as the angles
     if job.sc is not None:
-        def step():  # solve the shard + the library's one RCCL all-gather
-            job.sc.fabrik_device(job.dpts, dang, dit, derr, tol, max_iter, flags=flags)
+        def solve(p, a, i, e):  # solve the shard + the library's one RCCL all-gather
+            job.sc.fabrik_device(p, a, i, e, tol, max_iter, flags=flags)
+        batch = job.dpts
     else:
-        def step():
-            ctx.fabrik_solve_device(job.local_pts, dang, dit, None, tol, max_iter, flags=flags,
-                                    fk_err=derr)
+        def solve(p, a, i, e):
+            ctx.fabrik_solve_device(p, a, i, None, tol, max_iter, flags=flags, fk_err=e)
+        batch = job.local_pts
 
-    res = timed(ctx, step, args, world)
+    def step():
+        solve(batch, dang, dit, derr)
+
+    # the warm-up steps teach the work-order table on ANOTHER batch of the same
+    # distribution (seed 2), so the timed steps do not start from a table
+    # learned on their own points
+    wpts = torch.from_numpy(warm_batch(batch.shape[0])).cuda()
+    wang, wit, werr = torch.empty_like(dang), torch.empty_like(dit), torch.empty_like(derr)
+
+    def warm():
+        solve(wpts, wang, wit, werr)
+
+    ctx.fabrik_reset_order()  # start from a fresh context's table, whatever ran before
+    res = timed(ctx, step, args, world, warm=warm)
+    del wpts, wang, wit, werr
     st = ctx.stats_fetch()
     if job.sc is not None:
         res["gather_chunks"] = job.sc.info()[2]
@@ -522,17 +557,21 @@ def run_fabrik(job, args, tol=None, max_iter=None):
     local_iters = sum(int(dit[b:e].sum().item()) for b, e in _own_parts(job))
     k = res["kernels"].get("fabrik_iter_kernel")
     flops = FABRIK_FLOP_PER_ITER * local_iters
-    achieved = flops / (k / 1e3) if k else None
     pkey = "fabrik_iter_kernel" if (tol, max_iter) != (1e-5, 200) else \
         "fabrik_tol1e-5/fabrik_iter_kernel"
     traffic = load_traffic(args.traffic_file, pkey)
+    prof = profile_fields(args.traffic_file, pkey)
+    fr = roofline_fracs(flops, k, FP64_VALU_PEAK, prof)
+    achieved = fr.pop("_head")
     res["roofline"] = {"bound": "valu_fp64", "achieved": achieved / 1e12 if achieved else None,
                        "peak": FP64_VALU_PEAK / 1e12, "unit": "TFLOP/s",
                        "frac": achieved / FP64_VALU_PEAK if achieved else None,
+                       "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
+                       "frac_headline": fr["headline"],
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
                        "iterations_per_launch": local_iters,
-                       **profile_fields(args.traffic_file, pkey),
+                       **prof,
                        # the flop count prices a correctly rounded sqrt / division as
                        # one flop; the pipes say how busy the SIMDs actually are
                        "pipes": load_pipe(os.path.join(
@@ -568,12 +607,19 @@ def run_fk(job, args):
     res = timed(ctx, step, args, world)
     res["outputs"] = {"xyz": dxyz}
     k = res["kernels"].get("fk_kernel")
-    achieved = FK_BYTES_PER_POINT * n / (k / 1e3) if k else None
+    prof = profile_fields(args.traffic_file, "fk_kernel")
+    fr = roofline_fracs(FK_BYTES_PER_POINT * n, k, HBM_PEAK, prof)
+    achieved = fr.pop("_head")
     res["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None,
                        "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                        "frac": achieved / HBM_PEAK if achieved else None,
+                       "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
+                       "frac_headline": fr["headline"],
+                       "kernel_ms_note": "events bracket one launch of 1M points (its fixed "
+                                         "launch cost included); rocprof is the kernel's own "
+                                         "duration",
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
-                       **profile_fields(args.traffic_file, "fk_kernel"),
+                       **prof,
                        "kernel": "fk_kernel", "kernel_ms": k,
                        "algorithmic_bytes_per_point": FK_BYTES_PER_POINT,
                        "points_per_launch": n}
@@ -584,14 +630,20 @@ def run_fk(job, args):
     return res
 
 
-def timed(ctx, step, args, world):
+def warm_batch(n):
+    """The FABRIK warm-up batch: random_dist points of a seed no timed step uses."""
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    return random_dist(n, seed=2)
+
+
+def timed(ctx, step, args, world, warm=None):
     """W warm-up steps, one step timed per kernel, then K steps between barriers.
     Every wait on the steps is ctx.sync() first (ik_ctx_sync): bounded by the
     communicator's deadline at N > 1, so a stuck peer ends the run with
     IK_E_RCCL rather than hanging it; torch.cuda.synchronize() then returns at once."""
     import torch
     for _ in range(args.warmup):
-        step()
+        (warm or step)()
     ctx.sync()
     torch.cuda.synchronize()
     # per-kernel HIP-event durations of one representative step
@@ -624,29 +676,39 @@ def timed(ctx, step, args, world):
 
 
 def cold_steps(ctx, step, reps=3):
-    """The FABRIK step with the context's learned work order forgotten
-    (ik_fabrik_reset_order): the points go in point order, as on a fresh
-    context's first call (the CLI's and the RPC worker's first request), while
-    `value` is the warm steady state.  Median over `reps` (each cold call teaches
-    the table again, so each is preceded by a reset); scratch is already sized,
-    so this isolates the work order's effect."""
+    """The FABRIK step as a fresh context's first call makes it (the CLI's and
+    the RPC worker's first request, cli.py:269-287): the work-order table reset
+    to the library's built-in one for SixDOFRobot (ik_fabrik_reset_order), while
+    `value` is the warm steady state.  Beside it the same call from an EMPTY
+    table (point order: what a robot without a built-in table gets).  Median over
+    `reps` (each call teaches the table, so each is preceded by a reset); scratch
+    is already sized, so this isolates the work order's effect."""
     import torch
-    times = []
-    for _ in range(reps):
-        ctx.fabrik_reset_order()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        step()
-        e1.record()
-        ctx.sync()
-        torch.cuda.synchronize()
-        times.append(e0.elapsed_time(e1))
+
+    def run(reset):
+        times = []
+        for _ in range(reps):
+            reset()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            step()
+            e1.record()
+            ctx.sync()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        return times
+
+    prior = run(ctx.fabrik_reset_order)
+    empty = run(lambda: ctx.fabrik_order_set(None))
+    ctx.fabrik_reset_order()
     step()  # re-learn before anything else runs
     ctx.sync()
     torch.cuda.synchronize()
-    return {"ms": float(np.median(times)), "all_ms": times,
-            "note": "work-order table reset before each call (ik_fabrik_reset_order): point "
-                    "order, as a fresh context's first call; warm = ms_per_step"}
+    return {"ms": float(np.median(prior)), "all_ms": prior,
+            "empty_table_ms": float(np.median(empty)), "empty_table_all_ms": empty,
+            "note": "fresh-context call: work-order table reset to the built-in SixDOFRobot "
+                    "table before each call (ik_fabrik_reset_order); empty_table: point order; "
+                    "warm = ms_per_step (its table learned on a warm-up batch of another seed)"}
 
 
 def end_to_end(job, solve_host, args):

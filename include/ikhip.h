@@ -125,9 +125,18 @@ int ik_fabrik_solve_fk(ik_ctx *ctx, const double *pts, int64_t n, double tol, in
 
 /* Forget the context's learned FABRIK work order (the per-goal-cell cost table
  * the solves keep to start the hardest points first; DESIGN.md "Work order"):
- * the next solve runs in point order, as a fresh context's first call does.
- * Results never depend on it; only the launch's tail does. */
+ * the table goes back to a fresh context's -- for SixDOFRobot's chain the
+ * library's built-in one (learned on random_dist batches at tol 1e-3 / 100 and
+ * 1e-5 / 200; the first solve picks the one nearest its tolerance), for other
+ * chains empty, i.e. point order.  Results never depend on it; only the
+ * launch's tail does. */
 int ik_fabrik_reset_order(ik_ctx *ctx);
+/* The work-order table itself: n = 1024 cells, 1 + the largest recorded
+ * iteration count per goal cell (0 = unseen).  get waits for the context's last
+ * call and returns the count copied (or -ik_status); set with key NULL empties it
+ * (point order). */
+int ik_fabrik_order_get(ik_ctx *ctx, uint32_t *key, int n);
+int ik_fabrik_order_set(ik_ctx *ctx, const uint32_t *key, int n);
 
 /* Fabrik.calculate, kinematics/fabrik.py:44-67, batched over n goals for a chain
  * of nj (2..8) joints: init is n x nj x 3 (or nj x 3 shared by all goals when

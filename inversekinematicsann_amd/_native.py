@@ -41,7 +41,7 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_tail_reduce", "ik_fkhist_bin", "ik_fkhist_upper", "ik_fk_err_quantile",
                     "ik_ann_solve_sharded", "ik_fabrik_solve_sharded", "ik_host_alloc",
                     "ik_host_free", "ik_ctx_sync", "ik_comm_set_timeout",
-                    "ik_comm_loopback_stall")
+                    "ik_comm_loopback_stall", "ik_fabrik_order_get", "ik_fabrik_order_set")
 ANN_MODES = {"fp32": 0, "bf16x6": 1, "fp16x3": 2}
 
 
@@ -121,6 +121,8 @@ def load_library(path: str = LIB_PATH):
         L.ik_fabrik_solve_fk.argtypes = [vp, dp, i64, ctypes.c_double, i32, dp, ip, dp, dp,
                                          ctypes.c_int, st]
         L.ik_fabrik_reset_order.argtypes = [vp]
+        L.ik_fabrik_order_get.argtypes = [vp, vp, ctypes.c_int]
+        L.ik_fabrik_order_set.argtypes = [vp, vp, ctypes.c_int]
         L.ik_fabrik_calc.argtypes = [vp, ctypes.c_int, dp, dp, ctypes.c_int, dp, i64,
                                      ctypes.c_double, i32, dp, ip, ctypes.c_int, st]
         L.ik_ann_load.argtypes = [vp, ctypes.c_int, ip, ip, ctypes.POINTER(ctypes.c_void_p),
@@ -360,9 +362,23 @@ class Context:
         return s
 
     def fabrik_reset_order(self):
-        """Forget the learned FABRIK work order (ik_fabrik_reset_order): the next
-        solve starts cold, in point order, on the context's current stream."""
+        """Forget the learned FABRIK work order (ik_fabrik_reset_order): the table
+        a fresh context starts with (SixDOFRobot: the built-in prior; other chains:
+        empty, point order), on the context's current stream."""
         self._on_torch_stream(lambda: self._check(self.lib.ik_fabrik_reset_order(self.handle)))
+
+    def fabrik_order_get(self) -> np.ndarray:
+        """The work-order table (1024 uint32: 1 + largest recorded iterations per cell)."""
+        out = np.zeros(1024, np.uint32)
+        n = self.lib.ik_fabrik_order_get(self.handle, out.ctypes.data, out.size)
+        if n < 0:
+            raise NativeError(-n, self.lib.ik_last_error().decode())
+        return out
+
+    def fabrik_order_set(self, key=None):
+        """Replace the work-order table (None: empty, point order)."""
+        k = None if key is None else np.ascontiguousarray(key, np.uint32).reshape(1024)
+        self._check(self.lib.ik_fabrik_order_set(self.handle, _ptr(k), 0 if k is None else 1024))
 
     def fabrik_calc(self, dists, init, goals, tol=1e-3, max_iter=100):
         """Batched Fabrik.calculate; init n x nj x 3 or nj x 3 (shared)."""

@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "ik_fabrik_prior.h"
 #include "ik_internal.h"
 
 using namespace ikhip;
@@ -30,7 +31,51 @@ const double kDefaultLimits[6] = {0.0, 6.0, -6.0, 6.0, -3.0, 6.0};
 
 thread_local KTimer *g_kt = nullptr;
 
+static_assert(sizeof(FabPrior::key) == sizeof(FabOrderDev::key), "prior = one cost table");
+
+// The FABRIK work order's built-in tables (ik_fabrik_prior.h) describe
+// SixDOFRobot's chain (robot/robot.py:38-42): dh rows d, a, alpha and thetas[1:],
+// and the links.  theta_1 (dh[0]) is never read on the device.
+bool default_chain(const RobotDev &r) {
+  return std::memcmp(r.dh + 1, kDefaultDh + 1, 15 * sizeof(double)) == 0 &&
+         std::memcmp(r.links, kDefaultLinks, sizeof(kDefaultLinks)) == 0;
+}
+
+// The built-in table for a solve's (tol, max_iter): the nearest in log10(tol),
+// then max_iter; -1 without one.
+int prior_for(double tol, int max_iter) {
+  int best = -1;
+  double bd = 0.0;
+  for (int k = 0; k < kFabPriors; ++k) {
+    const double lt = tol > 0.0 ? std::log10(tol) : -30.0;
+    const double d = std::fabs(lt - std::log10(kFabPrior[k].tol)) * 1000.0 +
+                     std::fabs((double)(max_iter - kFabPrior[k].max_iter));
+    if (best < 0 || d < bd) {
+      best = k;
+      bd = d;
+    }
+  }
+  return best;
+}
+
 }  // namespace
+
+namespace ikapi {
+
+// A fresh table for the context's robot: the built-in one that suits (tol,
+// max_iter) when the chain is SixDOFRobot's, else empty (point order).
+int seed_order(ik_ctx *c, double tol, int max_iter) {
+  const int w = (c->fab_priors && default_chain(c->robot)) ? prior_for(tol, max_iter) : -1;
+  if (w >= 0)
+    IK_HIP(hipMemcpyAsync(c->fab_ord->key, c->fab_priors + (size_t)w * kOrdCells,
+                          sizeof(c->fab_ord->key), hipMemcpyDeviceToDevice, c->stream));
+  else
+    IK_HIP(hipMemsetAsync(c->fab_ord->key, 0, sizeof(c->fab_ord->key), c->stream));
+  c->fab_prior = w;
+  return IK_OK;
+}
+
+}  // namespace ikapi
 
 namespace ikhip {
 void kt_begin(const char *name, hipStream_t st) {
@@ -126,6 +171,15 @@ namespace ikapi {
 int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_iter, double *da,
                   int32_t *di, double *dj, double *dfe, bool limits, void *work, DevStats *S) {
   if (!S) S = c->d_stats;
+  // a table still holding a built-in prior takes the one for this call's
+  // tolerance; the solve then folds its own records in (learned from here on)
+  if (c->fab_prior >= 0 && n > 0) {
+    if (prior_for(tol, max_iter) != c->fab_prior) {
+      const int rc = seed_order(c, tol, max_iter);
+      if (rc) return rc;
+    }
+    c->fab_prior = -1;
+  }
   launch_reset_stats(S, c->stream);
   launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj, dfe, limits, work, S,
                       c->stream, c->fabrik_variant, c->fabrik_core, c->fab_ord, c->rconst,
@@ -178,6 +232,12 @@ int ik_ctx_create(int device, ik_ctx **out) {
   if (e == hipSuccess) e = hipHostMalloc(&c->h_stats, sizeof(DevStats), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMalloc(&c->fab_ord, sizeof(FabOrderDev));
   if (e == hipSuccess) e = hipMemset(c->fab_ord, 0, sizeof(FabOrderDev));
+  if (e == hipSuccess && kFabPriors > 0) {
+    e = hipMalloc(&c->fab_priors, sizeof(FabPrior::key) * kFabPriors);
+    for (int k = 0; k < kFabPriors && e == hipSuccess; ++k)
+      e = hipMemcpy(c->fab_priors + (size_t)k * kOrdCells, kFabPrior[k].key, sizeof(FabPrior::key),
+                    hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess) e = hipMalloc(&c->rconst, sizeof(RobotConstDev));
   if (e == hipSuccess) e = hipEventCreateWithFlags(&c->call_done, hipEventDisableTiming);
   c->stream = c->own_stream;
@@ -189,7 +249,10 @@ int ik_ctx_create(int device, ik_ctx **out) {
   std::memcpy(c->robot.links, kDefaultLinks, sizeof(kDefaultLinks));
   std::memcpy(c->robot.lim, kDefaultLimits, sizeof(kDefaultLimits));
   launch_robot_const(c->robot, c->rconst, c->stream);
-  e = hipStreamSynchronize(c->stream);
+  // a fresh context's work order: SixDOFRobot's built-in table for the
+  // reference's defaults (tol 1e-3, 100 iterations; FabrikInverseKinematics)
+  if (seed_order(c, 1e-3, 100) != IK_OK) e = hipErrorUnknown;
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   if (e == hipSuccess) e = hipGetLastError();
   if (e != hipSuccess) {
     (void)ik_ctx_destroy(c);
@@ -220,6 +283,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->fab_ord) (void)hipFree(c->fab_ord);
+  if (c->fab_priors) (void)hipFree(c->fab_priors);
   if (c->rconst) (void)hipFree(c->rconst);
   if (c->h_stats) (void)hipHostFree(c->h_stats);
   pipe_release(c);
@@ -259,7 +323,10 @@ int ik_set_robot(ik_ctx *c, const double *dh, const double *links, const double 
   if (chain || lim) {
     int rc = set_dev(c);
     if (rc) return rc;
-    if (chain) IK_HIP(hipMemsetAsync(c->fab_ord, 0, sizeof(FabOrderDev), c->stream));
+    if (chain) {  // another chain's costs: its own (built-in for SixDOFRobot's), or empty
+      const int rc = seed_order(c, 1e-3, 100);
+      if (rc) return rc;
+    }
     launch_robot_const(c->robot, c->rconst, c->stream);
     IK_HIP(hipGetLastError());
     // synchronous: later calls may run on another stream (ik_ctx_set_stream)
@@ -517,7 +584,29 @@ int ik_fabrik_reset_order(ik_ctx *c) {
   int rc = set_dev(c);
   if (rc) return rc;
   KtScope kts(c);  // ordered after the context's earlier calls, whatever their stream
-  IK_HIP(hipMemsetAsync(c->fab_ord, 0, sizeof(FabOrderDev), c->stream));
+  return seed_order(c, 1e-3, 100);
+}
+
+int ik_fabrik_order_get(ik_ctx *c, uint32_t *key, int n) {
+  if (!c || !key || n < kOrdCells) return -fail(IK_E_BADARG, "ik_fabrik_order_get: bad args");
+  if (set_dev(c)) return -IK_E_HIP;
+  if (hipStreamSynchronize(c->last_stream ? c->last_stream : c->stream) != hipSuccess ||
+      hipMemcpy(key, c->fab_ord->key, sizeof(c->fab_ord->key), hipMemcpyDeviceToHost) != hipSuccess)
+    return -fail(IK_E_HIP, "ik_fabrik_order_get: copy failed");
+  return kOrdCells;
+}
+
+int ik_fabrik_order_set(ik_ctx *c, const uint32_t *key, int n) {
+  if (!c || (key && n != kOrdCells)) return fail(IK_E_BADARG, "ik_fabrik_order_set: bad args");
+  int rc = set_dev(c);
+  if (rc) return rc;
+  KtScope kts(c);
+  IK_HIP(hipStreamSynchronize(c->stream));  // key may be a short-lived host buffer
+  if (key)
+    IK_HIP(hipMemcpy(c->fab_ord->key, key, sizeof(c->fab_ord->key), hipMemcpyHostToDevice));
+  else
+    IK_HIP(hipMemset(c->fab_ord->key, 0, sizeof(c->fab_ord->key)));
+  c->fab_prior = -1;
   return IK_OK;
 }
 

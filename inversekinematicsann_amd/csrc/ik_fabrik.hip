@@ -75,6 +75,159 @@ __device__ __forceinline__ void get_angles(const d3 J[4], double th[4], int &st)
   th[3] = (db > da) ? -(kPi - a4) : (kPi - a4);
 }
 
+// ---- the angles step through cheaper sequences ------------
+// Everything __get_angles compares or rounds -- the distances, the law-of-
+// cosines quotients, round(., 8), the C.x D.x and |B - D| > |B - m| tests -- must
+// keep the reference's bits (a different round(., 8) moves an angle by up to
+// 1e-4 near a straight joint).  sqrt_core / div_core give those bits on their
+// domains (ik_common.h).  Only the final math.acos / math.atan2 values leave
+// the kernel, and those need not be glibc's last bit (ocml's never were): the
+// angles are held to 1e-9 of the oracle (the north star's tolerance is 1e-5).
+// acos_fast / atan2_fast: polynomials fitted against mpmath (asin on [0, 1/2],
+// degree 11 in u^2, <= 2.1 ulp; atan on [0, tan(pi/8)], degree 10, <= 1 ulp), the
+// usual reductions, pi split in two parts.  ~40 VALU instructions each against
+// ~100 (ocml acos) and ~114 (ocml atan2).
+constexpr double kPio2Hi = 0x1.921fb54442d18p0, kPio2Lo = 0x1.1a62633145c07p-54;
+constexpr double kPio4Hi = 0x1.921fb54442d18p-1, kPio4Lo = 0x1.1a62633145c07p-55;
+constexpr double kPiHi = 0x1.921fb54442d18p1, kPiLo = 0x1.1a62633145c07p-53;
+
+// asin(u) for u in [0, 1/2]: u + u z P(z), z = u^2 (z passed in)
+__device__ __forceinline__ double asin_small(double u, double z) {
+  double p = 0x1.c4e4e17088d7fp-6;
+  p = __builtin_fma(p, z, -0x1.478579af5a664p-7);
+  p = __builtin_fma(p, z, 0x1.fe14951c32a4cp-7);
+  p = __builtin_fma(p, z, 0x1.0524bf7ebc431p-7);
+  p = __builtin_fma(p, z, 0x1.83eb350c10662p-7);
+  p = __builtin_fma(p, z, 0x1.c89fb23c062d2p-7);
+  p = __builtin_fma(p, z, 0x1.1c5717f04e8d6p-6);
+  p = __builtin_fma(p, z, 0x1.6e8b4bd3059d9p-6);
+  p = __builtin_fma(p, z, 0x1.f1c71e76e5bd8p-6);
+  p = __builtin_fma(p, z, 0x1.6db6db6aaeb82p-5);
+  p = __builtin_fma(p, z, 0x1.3333333335124p-4);
+  p = __builtin_fma(p, z, 0x1.555555555555fp-3);
+  return __builtin_fma(u * z, p, u);
+}
+
+// atan(t) for |t| <= tan(pi/8): t + t s P(s), s = t^2
+__device__ __forceinline__ double atan_small(double t) {
+  const double s = t * t;
+  double p = -0x1.f318cc05bca37p-7;
+  p = __builtin_fma(p, s, 0x1.2487560b8b924p-5);
+  p = __builtin_fma(p, s, -0x1.959b5ed0b32b2p-5);
+  p = __builtin_fma(p, s, 0x1.dd91ab8788317p-5);
+  p = __builtin_fma(p, s, -0x1.10d3fc8f710cbp-4);
+  p = __builtin_fma(p, s, 0x1.3b0f4916f8726p-4);
+  p = __builtin_fma(p, s, -0x1.745ce3b26915fp-4);
+  p = __builtin_fma(p, s, 0x1.c71c705fa87fap-4);
+  p = __builtin_fma(p, s, -0x1.24924921fc848p-3);
+  p = __builtin_fma(p, s, 0x1.99999999958a3p-3);
+  p = __builtin_fma(p, s, -0x1.5555555555541p-2);
+  return __builtin_fma(t * s, p, t);
+}
+
+// math.acos on [-1, 1] (NaN outside, and for NaN): |x| <= 1/2 as pi/2 -+ asin|x|,
+// else 2 asin(sqrt((1 - |x|) / 2)) (x > 0) or pi minus it; 1 - |x| is exact there.
+__device__ __forceinline__ double acos_fast(double x) {
+  const double ax = fabs(x);
+  const bool small = ax <= 0.5;
+  const double zl = (1.0 - ax) * 0.5;  // 0 or >= 2^-54: sqrt_core's domain or 0
+  const double z = small ? x * x : zl;
+  const double u = small ? ax : (zl > 0.0 ? sqrt_core(zl) : 0.0);
+  const double p = asin_small(u, z);
+  const double r_small = x >= 0.0 ? kPio2Hi - (p - kPio2Lo) : kPio2Hi + (p + kPio2Lo);
+  const double r_large = x > 0.0 ? 2.0 * p : kPiHi - (2.0 * p - kPiLo);
+  const double r = small ? r_small : r_large;
+  return ax <= 1.0 ? r : __builtin_nan("");
+}
+
+// math.atan2 where both |x| and |y| are in [2^-100, 2^100] (div_core's domain);
+// the caller sends zeros, non-finite and extreme values to the library's atan2.
+__device__ __forceinline__ double atan2_fast(double y, double x) {
+  const double ax = fabs(x), ay = fabs(y);
+  const bool swap = ay > ax;
+  const double r = div_core(swap ? ax : ay, swap ? ay : ax);  // [0, 1]
+  const bool red = r > 0x1.a827999fcef32p-2;  // tan(pi/8): atan r = pi/4 + atan((r-1)/(r+1))
+  const double t = red ? div_core(r - 1.0, r + 1.0) : r;
+  double a = atan_small(t);
+  a = red ? kPio4Hi + (a + kPio4Lo) : a;
+  a = swap ? kPio2Hi - (a - kPio2Lo) : a;
+  a = x < 0.0 ? kPiHi - (a - kPiLo) : a;
+  return copysign(a, y);
+}
+
+__device__ __forceinline__ bool in_div_domain(double v) {
+  const double a = fabs(v);
+  return a >= 0x1p-100 && a <= 0x1p100;
+}
+
+// dist3 through sqrt_core (same bits where dom stays below kCoreDom)
+__device__ __forceinline__ double dist3c(d3 a, d3 b, uint32_t &dom) {
+  const double x = dist3_sq(a, b);
+  dom = max(dom, sqrt_core_dom(x));
+  return sqrt_core(x);
+}
+
+// round(v, 8) (py_round8) with the final k / 1e8 through div_core
+__device__ __forceinline__ double py_round8_core(double v, bool &ok) {
+  const double s = 1e8;
+  const double p = v * s;
+  if (!isfinite(p)) return v;
+  const double e = fma(v, s, -p);
+  const double fl = floor(p);
+  double k;
+  if (p - fl == 0.5) {
+    k = (e > 0) ? fl + 1.0 : ((e < 0) ? fl : rint(p));
+  } else {
+    k = rint(p);
+  }
+  ok = ok && (k == 0.0 || in_div_domain(k));
+  double r = div_core(k, s);
+  if (r == 0.0) r = copysign(0.0, v);
+  return r;
+}
+
+// __get_angles (inverse.py:54-112) through the core sequences; returns false
+// (and the caller runs get_angles) when some radicand or quotient leaves their
+// domains -- coincident joints, a zero divisor, non-finite joints -- or the
+// effector's x or y is zero or extreme (atan2's special cases).
+__device__ __forceinline__ bool get_angles_core(const d3 J[4], double th[4], int &st) {
+  const d3 A = {0.0, 0.0, 0.0};
+  const d3 B = J[0], C = J[1], D = J[2], E = J[3];
+  uint32_t dom = 0;
+  bool ok = in_div_domain(E.x) && in_div_domain(E.y);
+  const double ab = dist3c(A, B, dom), bc = dist3c(B, C, dom), cd = dist3c(C, D, dom),
+               de = dist3c(D, E, dom);
+  const double ac = dist3c(A, C, dom);
+  auto quot = [&](double num, double den) {
+    ok = ok && (num == 0.0 || in_div_domain(num)) && in_div_domain(den);
+    return div_core(num, den);
+  };
+  auto acos_py = [&](double v) {
+    if (v > 1.0 || v < -1.0) set_err(st, IK_E_DOMAIN);
+    return acos_fast(v);
+  };
+  double num = (sq(ab) + sq(bc)) - sq(ac);
+  double den = 2 * ab * bc;
+  const double a2 = acos_py(py_round8_core(quot(num, den), ok));
+  th[1] = (C.x * D.x < 0) ? ((3 * kPi / 2) - a2) : -(kPi / 2 - a2);
+  const double bd = dist3c(B, D, dom);
+  num = (sq(bc) + sq(cd)) - sq(bd);
+  den = 2 * bc * cd;
+  const double a3 = acos_py(py_round8_core(quot(num, den), ok));
+  th[2] = -(kPi - a3);
+  const double ce = dist3c(C, E, dom);
+  num = (sq(cd) + sq(de)) - sq(ce);
+  den = 2 * cd * de;
+  const double a4 = acos_py(py_round8_core(quot(num, den), ok));
+  // get_point_between(C, E, |C - E| / 2): |C - E| is ce again (the radicand squares
+  // E - C = -(C - E) exactly) and (ce / 2) / ce is exactly 0.5 for a ce in the domain
+  const d3 m = {C.x + (0.5 * (E.x - C.x)), C.y + (0.5 * (E.y - C.y)), C.z + (0.5 * (E.z - C.z))};
+  const double da = dist3c(B, m, dom);
+  th[3] = (bd > da) ? -(kPi - a4) : (kPi - a4);  // db = |B - D| = bd
+  // th[0] = atan2_fast(E.y, E.x): by the caller, after the fallback pass
+  return ok && dom < kCoreDom;
+}
+
 // Seed pose, inverse.py:123-130: FK of [atan2(y, x), thetas[1:]] (the
 // reference writes theta_1 into dh_matrix[0][0] and runs fkine on that row),
 // through the per-robot constants (seed_chain; same bits as fk_chain).
@@ -199,10 +352,11 @@ __device__ __forceinline__ bool outside_rc(RcConst k, d3 g) {
   return outside(lim, g.x, g.y, g.z);
 }
 
-__device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const d3 J[4], d3 g,
-                                             int it, int st, LaneAcc &acc) {
-  double th[4] = {__builtin_nan(""), __builtin_nan(""), __builtin_nan(""), __builtin_nan("")};
-  if (st == IK_OK) get_angles(J, th, st);
+// What the call reports about one finished point once its angles are known:
+// angles, iterations, joints, the FK round trip (cli.py:54-61) and the per-lane
+// sums of the batch stats.
+__device__ __forceinline__ void commit_point(const FabArgs &a, int64_t i, const d3 J[4], d3 g,
+                                             int it, int st, const double th[4], LaneAcc &acc) {
   if (st != IK_OK) record_error(a.S, i, st);
   double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
   o[0] = make_double2(th[0], th[1]);
@@ -229,6 +383,44 @@ __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const 
   }
 }
 
+// The angles step of one finished point (inverse.py:136 __get_angles): the core
+// sequences (get_angles_core); a lane outside their domains is flagged (redo)
+// and the whole wave then runs the general get_angles for the flagged lanes in
+// a pass of its own, so the general code's registers are never live beside the
+// fast path's.  has: the lane holds a point; st: its status so far.
+#ifndef IKHIP_FAB_FAST_ANGLES  // 0: the general get_angles for every point (A/B builds)
+#define IKHIP_FAB_FAST_ANGLES 1
+#endif
+template <class Joints>
+__device__ __forceinline__ void angles_step(bool has, Joints joints, int &st, double th[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) th[k] = __builtin_nan("");
+  bool redo = false, fast = false;
+  if (IKHIP_FAB_FAST_ANGLES && has && st == IK_OK) {
+    d3 J[4];
+    joints(J);
+    int sf = IK_OK;
+    fast = get_angles_core(J, th, sf);
+    redo = !fast;
+    if (fast) st = sf;
+  }
+  if (!IKHIP_FAB_FAST_ANGLES && has && st == IK_OK) redo = true;  // (A/B build: general only)
+  if (__any(redo)) {  // wave-uniform and rare: coincident joints, zero divisors, x = 0 or y = 0
+    if (redo) {
+      d3 J[4];
+      joints(J);
+      get_angles(J, th, st);
+    }
+  }
+  // theta_1 (inverse.py:60) last: kept out of the fast pass, whose registers
+  // then fit beside the general pass's without spilling
+  if (fast) {
+    d3 J[4];
+    joints(J);
+    th[0] = atan2_fast(J[3].y, J[3].x);
+  }
+}
+
 // ------------------------------------------------------------- simple ----
 // One point per lane, no refill: the test variant (IKHIP_FABRIK_VARIANT=0) and
 // the solves whose loop runs no iteration at all (max_iter 0, tol >= 1) or whose
@@ -236,14 +428,14 @@ __device__ __forceinline__ void finish_point(const FabArgs &a, int64_t i, const 
 __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   LaneAcc acc;
+  d3 g = {0.0, 0.0, 0.0}, J[4] = {};
+  int st = IK_OK, it = 0;
   if (i < a.n) {
-    d3 g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
+    g = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
     if (a.check_limits && outside(a.r.lim, g.x, g.y, g.z))
       atomicMin(&a.S->first_oob, (unsigned long long)i);
-    d3 J[4];
-    int st = seed_pose(a.rc, g, J);
+    st = seed_pose(a.rc, g, J);
     double se = 1.0, ge = 1.0;
-    int it = 0;
     if (st == IK_OK) {
       while (((se > a.tol2) || (ge > a.tol2)) && (a.max_iter > it)) {
         fabrik_step4(J[0], J[1], J[2], J[3], g, a.r.links, se, ge, st);
@@ -251,8 +443,13 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
         if (st != IK_OK) break;
       }
     }
-    finish_point(a, i, J, g, it, st, acc);
   }
+  double th[4];
+  angles_step(i < a.n, [&](d3 *o) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = J[k];
+  }, st, th);
+  if (i < a.n) commit_point(a, i, J, g, it, st, th, acc);
   block_iter_stats_acc(a.S, acc.sum_it, acc.capped, acc.max_it);
   if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
 }
@@ -487,14 +684,24 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
                                            LaneAcc &acc) {
   prio_raise();
   __builtin_amdgcn_wave_barrier();
-  if (lane < cnt) {
-    d3 J[4];
+  const bool has = lane < cnt;
+  // the joints from the ring each time they are needed (LDS reads are cheap; the
+  // barrier keeps the compiler from holding them in registers across the step)
+  auto joints = [&](d3 *J) {
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       J[k] = {R.j[3 * k][lane], R.j[3 * k + 1][lane], R.j[3 * k + 2][lane]};
+  };
+  int st = has ? R.st[lane] : IK_OK;
+  double th[4];
+  angles_step(has, joints, st, th);
+  if (has) {
+    d3 J[4];
+    joints(J);
     const int64_t i = R.idx[lane];
     const int it = R.it[lane];
-    finish_point(a, i, J, {R.g[0][lane], R.g[1][lane], R.g[2][lane]}, it, R.st[lane], acc);
+    commit_point(a, i, J, {R.g[0][lane], R.g[1][lane], R.g[2][lane]}, it, st, th, acc);
     if constexpr (ORD) {
       if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
         a.ord->sample[i / kOrdSample] = ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) |

@@ -110,6 +110,8 @@ struct ik_ctx {
   ikhip::KTimer kt;
   unsigned long long *dbg = nullptr;     // diagnostic stamp buffer (ik_ctx_set_debug)
   ikhip::FabOrderDev *fab_ord = nullptr;  // FABRIK work-order cost table (learned per robot)
+  unsigned int *fab_priors = nullptr;     // device copies of the built-in tables (ik_fabrik_prior.h)
+  int fab_prior = -1;  // the built-in table fab_ord holds untouched (index), -1 learned / empty
   ikhip::RobotConstDev *rconst = nullptr;  // FABRIK seed-pose constants of the robot
   IkComm comm;
   IkPipe pipe;
@@ -160,6 +162,9 @@ int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_it
                   ikhip::DevStats *S = nullptr);
 int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bool limits,
                ikhip::DevStats *S = nullptr);
+// The FABRIK work order of a fresh table (ik_api.cpp): the built-in prior for
+// (tol, max_iter) when the robot is SixDOFRobot's chain, else empty.
+int seed_order(ik_ctx *c, double tol, int max_iter);
 // FABRIK host-pointer solves whose arrays are all pinned (ik_host_alloc) and large enough:
 // chunked H2D / solve / D2H on three streams (ik_pipe.cpp).
 bool pipeline_wanted(ik_ctx *c, int64_t n, std::initializer_list<const void *> ptrs);

@@ -1097,6 +1097,9 @@ int ik_ann_solve_sharded(ik_ctx *c, const double *pts, int64_t n, float *ang, do
   double *dfk = fk_err;
   HostStage hs;
   if (!dev) {
+    // pageable host copies wait for the stream: the previous call's end first
+    if (c->comm.ev_end_set && (rc = comm_wait(c, c->comm.ev_end, "the previous sharded call")))
+      return rc;
     const int rb[1] = {16};
     char *unused = nullptr;
     if ((rc = host_stage(c, P, n, rb, 1, fk_err != nullptr, 0, &hs, &unused))) return rc;
@@ -1112,6 +1115,9 @@ int ik_ann_solve_sharded(ik_ctx *c, const double *pts, int64_t n, float *ang, do
   });
   if (rc) return rc;
   if (!dev) {
+    // copies into pageable host memory block the thread until the stream
+    // reaches them: first the bounded wait for the gathers
+    if ((rc = comm_wait(c, c->comm.ev_end, "the sharded call"))) return rc;
     char *ho[1] = {reinterpret_cast<char *>(ang)};
     if ((rc = host_results_out(c, P, R, 1, ho, hs.fk, fk_err))) return rc;
   }
@@ -1150,6 +1156,8 @@ int ik_fabrik_solve_sharded(ik_ctx *c, const double *pts, int64_t n, double tol,
   char *work = nullptr;
   HostStage hs;
   if (!dev) {
+    if (c->comm.ev_end_set && (rc = comm_wait(c, c->comm.ev_end, "the previous sharded call")))
+      return rc;
     const int rb[2] = {32, 4};
     if ((rc = host_stage(c, P, n, rb, nreg, fk_err != nullptr, b_work, &hs, &work))) return rc;
     if ((rc = host_points_in(c, P, pts, hs.pts))) return rc;
@@ -1169,6 +1177,7 @@ int ik_fabrik_solve_sharded(ik_ctx *c, const double *pts, int64_t n, double tol,
   });
   if (rc) return rc;
   if (!dev) {
+    if ((rc = comm_wait(c, c->comm.ev_end, "the sharded call"))) return rc;
     char *ho[2] = {reinterpret_cast<char *>(ang), reinterpret_cast<char *>(iters)};
     if ((rc = host_results_out(c, P, R, nreg, ho, hs.fk, fk_err))) return rc;
   }

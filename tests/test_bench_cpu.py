@@ -154,3 +154,14 @@ def test_gather_check_parts_of_the_next_rank():
     bad[parts[-1][1] - 1, 3] += 1
     res = bench.gather_check(job, {"ang": bad}, lambda b, e: {"ang": full[b:e].copy()})
     assert not res["bit_exact"] and res["mismatched_rows"] == 1
+
+
+def test_roofline_fracs_headline_the_lower():
+    """VERDICT r03 #4: both the event and the rocprof figure, the lower one headlined."""
+    import bench
+    fr = bench.roofline_fracs(100.0, 2000.0, 1000.0, {"rocprof_avg_ms": 2500.0})
+    assert abs(fr["frac_events"] - 0.05) < 1e-12 and abs(fr["frac_rocprof"] - 0.04) < 1e-12
+    assert fr["headline"] == "rocprof" and abs(fr["_head"] - 40.0) < 1e-9
+    fr = bench.roofline_fracs(100.0, 2000.0, 1000.0, {})
+    assert fr["headline"] == "events" and fr["frac_rocprof"] is None
+    assert bench.roofline_fracs(100.0, None, 1000.0, {})["headline"] is None

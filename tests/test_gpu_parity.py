@@ -447,13 +447,52 @@ def test_fabrik_work_order_is_invisible():
                 else:
                     assert np.array_equal(ang, first[0], equal_nan=True)
                     assert np.array_equal(it, first[1])
-        # a forgotten table (ik_fabrik_reset_order: point order again) changes nothing
+        # a forgotten table (ik_fabrik_reset_order: the built-in one again) and an
+        # empty one (point order) change nothing
         c.fabrik_reset_order()
+        ang, it, _, _ = c.fabrik_solve(big, 1e-3, 100)
+        assert np.array_equal(ang, first[0], equal_nan=True) and np.array_equal(it, first[1])
+        c.fabrik_order_set(None)
         ang, it, _, _ = c.fabrik_solve(big, 1e-3, 100)
         assert np.array_equal(ang, first[0], equal_nan=True) and np.array_equal(it, first[1])
         ref_ang, ref_it, _, _ = O.fabrik_ikine(big[:8192], 1e-3, 100)
         assert np.array_equal(first[1][:8192], ref_it)  # bit-exact iteration counts
         assert np.abs(first[0][:8192] - ref_ang).max() <= 1e-9
+    finally:
+        c.close()
+
+
+def test_fabrik_builtin_work_order_table():
+    """a fresh context of SixDOFRobot's chain starts from the
+    library's built-in cost table (the tol 1e-3 / 100 one); its first solve at
+    tol 1e-5 / 200 swaps in that tolerance's table before it learns; reset
+    restores the built-in one; another chain starts empty (point order) and
+    going back to SixDOFRobot's restores the built-in table."""
+    import json
+    import os
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "profiles", "r04", "fabrik_prior_tables.json")) as f:
+        tabs = {k: np.array(v, np.uint32) for k, v in json.load(f)["tables"].items()}
+    c = _native.Context(0)
+    try:
+        assert np.array_equal(c.fabrik_order_get(), tabs["0.001/100"])
+        pts = random_dist(300, seed=8)
+        c.fabrik_solve(pts, 1e-5, 200)
+        t = c.fabrik_order_get()  # the 1e-5 table with this call's records folded in
+        assert np.all(t >= tabs["1e-05/200"] - (tabs["1e-05/200"] >> 3))
+        assert not np.array_equal(t, tabs["0.001/100"])
+        c.fabrik_reset_order()
+        assert np.array_equal(c.fabrik_order_get(), tabs["0.001/100"])
+        c.fabrik_order_set(None)
+        assert not c.fabrik_order_get().any()
+        c.set_robot(np.array([[0.0, np.pi / 2, 0, 0], [2, 0, 0, 0], [0, 2, 2, 1.5],
+                              [np.pi / 2, 0, 0, 0]]), links=[2, 2, 2, 1.5])
+        assert not c.fabrik_order_get().any()
+        c.set_robot(np.array([[0.0, np.pi / 2, 0, 0], [2, 0, 0, 0], [0, 2, 2, 2],
+                              [np.pi / 2, 0, 0, 0]]), links=[2, 2, 2, 2])
+        assert np.array_equal(c.fabrik_order_get(), tabs["0.001/100"])
     finally:
         c.close()
 
