@@ -139,8 +139,10 @@ int ik_fabrik_order_get(ik_ctx *ctx, uint32_t *key, int n);
 int ik_fabrik_order_set(ik_ctx *ctx, const uint32_t *key, int n);
 
 /* Fabrik.calculate, kinematics/fabrik.py:44-67, batched over n goals for a chain
- * of nj (2..8) joints: init is n x nj x 3 (or nj x 3 shared by all goals when
- * init_shared != 0), goals n x 3 -> joints n x nj x 3, iters n (nullable). */
+ * of nj (1..2^20) joints: init is n x nj x 3 (or nj x 3 shared by all goals when
+ * init_shared != 0), goals n x 3 -> joints n x nj x 3, iters n (nullable).
+ * 2..8 joints run with the chain in registers; other lengths keep it in the
+ * joints output row (same arithmetic, same bits). */
 int ik_fabrik_calc(ik_ctx *ctx, int nj, const double *dists, const double *init,
                    int init_shared, const double *goals, int64_t n, double tol,
                    int32_t max_iter, double *joints, int32_t *iters, int flags,
@@ -151,8 +153,13 @@ int ik_fabrik_calc(ik_ctx *ctx, int nj, const double *dists, const double *init,
  * Dense layers, dims[0..n_layers] (dims[0] == 3, dims[n_layers] == 4), acts[l]
  * one of IK_ACT_*, W[l] host float32 [dims[l]][dims[l+1]] row-major (the Keras
  * kernel layout, x @ W + b), b[l] host float32 [dims[l+1]], and the two
- * StandardScalers (ann.py:83-84).  Widths up to 1024 (models wider than 512 run
- * the fp32 kernel whatever ik_ann_set_mode says). */
+ * StandardScalers (ann.py:83-84).  Up to 4096 layers of widths up to 16384.
+ * Up to 24 layers of widths up to 1024 run the fused kernel (one launch, the
+ * activations in LDS); models wider than 512 there run its fp32 build whatever
+ * ik_ann_set_mode says.  Deeper or wider models run layer at a time with the
+ * activations in HBM (fp32 MFMA, one launch per layer and chunk of points,
+ * still one ik_ann_solve call; ik_ann_set_mode does not apply), in chunks whose
+ * two activation buffers fit IKHIP_ANN_ACT_MB (default 1024 MiB). */
 int ik_ann_load(ik_ctx *ctx, int n_layers, const int32_t *dims, const int32_t *acts,
                 const float *const *W, const float *const *b, const double *x_mean,
                 const double *x_scale, const double *y_mean, const double *y_scale);

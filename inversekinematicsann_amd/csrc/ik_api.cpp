@@ -192,6 +192,32 @@ int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bo
                DevStats *S) {
   if (!S) S = c->d_stats;
   launch_reset_stats(S, c->stream);
+  if (c->ann_big) {
+    // two activation buffers of chunk x ld floats within IKHIP_ANN_ACT_MB (default
+    // 1024 MiB; at least one 128-row tile), grown on demand
+    if (n <= 0) return IK_OK;
+    const char *bv = getenv("IKHIP_ANN_ACT_MB");  // (read per call: tests shrink it)
+    long long budget_mb = (bv && *bv) ? atoll(bv) : 1024;
+    if (budget_mb <= 0) budget_mb = 1024;
+    const size_t ld = ann_big_ld(c->ann_bigm);
+    int64_t rows = ann_big_rows(c->ann_bigm, (size_t)budget_mb << 20);
+    if (rows < 128) rows = 128;
+    const int64_t n128 = (n + 127) / 128 * 128;
+    if (rows > n128) rows = n128;
+    const size_t bytes = 2 * (size_t)rows * ld * sizeof(float);
+    if (bytes > c->ann_act_bytes) {
+      IK_HIP(hipStreamSynchronize(c->stream));
+      if (c->ann_act) IK_HIP(hipFree(c->ann_act));
+      c->ann_act = nullptr;
+      c->ann_act_bytes = 0;
+      IK_HIP(hipMalloc(&c->ann_act, bytes));
+      c->ann_act_bytes = bytes;
+    }
+    launch_ann_big(c->ann_bigm, c->robot, dp, n, da, de, limits, S, c->stream,
+                   static_cast<float *>(c->ann_act), rows);
+    IK_HIP(hipGetLastError());
+    return IK_OK;
+  }
   AnnModelDev m = c->ann;
   m.xmode = c->ann_mode;
   for (int l = 0; l < m.n_layers; ++l) {
@@ -280,6 +306,7 @@ int ik_ctx_destroy(ik_ctx *c) {
   (void)hipStreamSynchronize(c->stream);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->ann_buf) (void)hipFree(c->ann_buf);
+  if (c->ann_act) (void)hipFree(c->ann_act);
   if (c->d_stats) (void)hipFree(c->d_stats);
   if (c->dbg) (void)hipFree(c->dbg);
   if (c->fab_ord) (void)hipFree(c->fab_ord);
@@ -614,9 +641,10 @@ int ik_fabrik_calc(ik_ctx *c, int nj, const double *dists, const double *init,
                    int init_shared, const double *goals, int64_t n, double tol,
                    int32_t max_iter, double *joints, int32_t *iters, int flags,
                    ik_stats *stats) {
-  if (!c || nj < 2 || nj > 8 || !dists || n < 0 || (n > 0 && (!init || !goals || !joints)) ||
-      max_iter < 0)
-    return fail(IK_E_BADARG, "ik_fabrik_calc: bad args (nj must be 2..8)");
+  if (!c || nj < 1 || nj > kCalcMaxJoints || !dists || n < 0 ||
+      (n > 0 && (!init || !goals || !joints)) || max_iter < 0)
+    return fail(IK_E_BADARG, "ik_fabrik_calc: bad args (nj must be 1.." +
+                                 std::to_string(kCalcMaxJoints) + ")");
   if ((flags & IK_F_ASYNC) && !(flags & IK_F_DEVICE))
     return fail(IK_E_BADARG, "IK_F_ASYNC requires IK_F_DEVICE");
   int rc = set_dev(c);
@@ -666,15 +694,19 @@ int ik_fabrik_calc(ik_ctx *c, int nj, const double *dists, const double *init,
 int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *acts,
                 const float *const *W, const float *const *b, const double *x_mean,
                 const double *x_scale, const double *y_mean, const double *y_scale) {
-  if (!c || n_layers < 1 || n_layers > kAnnMaxLayers || !dims || !acts || !W || !b ||
+  if (!c || n_layers < 1 || n_layers > kAnnBigMaxLayers || !dims || !acts || !W || !b ||
       !x_mean || !x_scale || !y_mean || !y_scale)
-    return fail(IK_E_BADARG, "ik_ann_load: bad args");
+    return fail(IK_E_BADARG, "ik_ann_load: bad args (1.." + std::to_string(kAnnBigMaxLayers) +
+                                 " layers)");
   if (dims[0] != 3 || dims[n_layers] != 4)
     return fail(IK_E_BADARG, "ik_ann_load: the model must map 3 inputs to 4 outputs");
   for (int l = 0; l <= n_layers; ++l)
-    if (dims[l] < 1 || dims[l] > kAnnMaxWidth)
+    if (dims[l] < 1 || dims[l] > kAnnBigMaxWidth)
       return fail(IK_E_BADARG, "ik_ann_load: layer widths must be 1.." +
-                                   std::to_string(kAnnMaxWidth));
+                                   std::to_string(kAnnBigMaxWidth));
+  // past the fused kernel's caps: the layered path (fp32, activations through HBM)
+  bool big = n_layers > kAnnMaxLayers;
+  for (int l = 0; l <= n_layers; ++l) big = big || dims[l] > kAnnMaxWidth;
   for (int l = 0; l < n_layers; ++l)
     if (acts[l] < IK_ACT_LINEAR || acts[l] > IK_ACT_SIGMOID)
       return fail(IK_E_BADARG, "ik_ann_load: unsupported activation code");
@@ -686,7 +718,7 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   std::vector<size_t> woff(n_layers), boff(n_layers), xoff(n_layers, 0), hoff(n_layers, 0);
   std::vector<int> hexp(n_layers, 0);
   // models wider than 512 run the wide fp32 kernel only: no split operands
-  bool wide = false;
+  bool wide = big;
   for (int l = 0; l <= n_layers; ++l) wide = wide || dims[l] > 512;
   auto splittable = [&](int l) { return !wide && l > 0 && (dims[l + 1] + 31) / 32 > 1; };
   // fp16x3 also needs a bounded layer input: the layer before is tanh or sigmoid
@@ -729,10 +761,30 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   c->ann_loaded = false;
   IK_HIP(hipMalloc(&c->ann_buf, total));
   IK_HIP(hipMemcpy(c->ann_buf, host.data(), total, hipMemcpyHostToDevice));
+  char *base = static_cast<char *>(c->ann_buf);
+  c->ann_big = big;
+  c->ann_bigm.layers.clear();
+  if (big) {
+    AnnBigModel &bm = c->ann_bigm;
+    for (int l = 0; l < n_layers; ++l)
+      bm.layers.push_back({(dims[l] + 7) / 8 * 8, (dims[l + 1] + 31) / 32 * 32, acts[l],
+                           reinterpret_cast<const float *>(base + woff[l]),
+                           reinterpret_cast<const float *>(base + boff[l])});
+    for (int i = 0; i < 3; ++i) {
+      bm.xm[i] = x_mean[i];
+      bm.xs[i] = x_scale[i];
+    }
+    for (int i = 0; i < 4; ++i) {
+      bm.ym[i] = y_mean[i];
+      bm.ys[i] = y_scale[i];
+    }
+    std::memset(&c->ann, 0, sizeof(c->ann));
+    c->ann_loaded = true;
+    return IK_OK;
+  }
   AnnModelDev &m = c->ann;
   std::memset(&m, 0, sizeof(m));
   m.n_layers = n_layers;
-  char *base = static_cast<char *>(c->ann_buf);
   for (int l = 0; l < n_layers; ++l) {
     m.kp[l] = (dims[l] + 7) / 8 * 8;
     m.np[l] = (dims[l + 1] + 31) / 32 * 32;

@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include <cmath>
+#include <vector>
 
 #include "../../include/ikhip.h"
 
@@ -507,6 +508,8 @@ void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, dou
 // FK of a chain of nj (2..kFkMaxJoints) joints; dh: device 4 x nj, mats nullable
 // n x nj x 16 (2..8 unrolled, longer chains a run-time joint loop).
 constexpr int kFkMaxJoints = 1024;
+// Fabrik.calculate's chain length bound (ik_fabrik_calc)
+constexpr int kCalcMaxJoints = 1 << 20;
 void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double *xyz,
                  double *mats, DevStats *S, hipStream_t st);
 // FABRIK work order (ik_fabrik.hip "Work order"): per context, the largest
@@ -566,4 +569,27 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
 void launch_ann_wide(const AnnModelDev &m, const RobotDev &r, const double *pts, int64_t n,
                      float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
                      unsigned long long *dbg);
+
+// Models outside the fused kernel's caps (more than kAnnMaxLayers layers or a
+// layer wider than kAnnMaxWidth): layer at a time through HBM (ik_ann_big.hip),
+// fp32 only.  Bounds of that path:
+constexpr int kAnnBigMaxLayers = 4096;
+constexpr int kAnnBigMaxWidth = 16384;
+struct AnnBigLayer {
+  int kp, np, act;   // padded in-dim (multiple of 8), padded out-dim (multiple of 32)
+  const float *wp;   // packed weights (ann_pack_layer order)
+  const float *bias; // np floats, zero past the layer's width
+};
+struct AnnBigModel {
+  std::vector<AnnBigLayer> layers;
+  double xm[3], xs[3], ym[4], ys[4];
+};
+// floats per activation row (the widest padded layer, at least 8)
+size_t ann_big_ld(const AnnBigModel &m);
+// rows per chunk that fit two activation buffers in act_bytes (multiple of 128)
+int64_t ann_big_rows(const AnnBigModel &m, size_t act_bytes);
+// act: 2 * chunk_rows * ann_big_ld(m) floats
+void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, int64_t n,
+                    float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
+                    float *act, int64_t chunk_rows);
 }  // namespace ikhip

@@ -1243,6 +1243,59 @@ __global__ __launch_bounds__(256) void fabrik_calc_kernel(const double *dists_in
   block_iter_stats(S, valid, it, max_iter);
 }
 
+// Any chain length (1 joint up, fabrik.py:44-67 takes any len(init) ==
+// len(dists)): the chain lives in the lane's output row instead of registers.
+// The backward pass writes B[k] over cur[k] (cur[k] is read only to form B[k]),
+// and the forward pass writes the new cur[k] over B[k] (read only to form it),
+// so one nj x 3 row per point holds both passes.  Same point_between calls in the
+// same order as the unrolled kernel: the same bits.
+__global__ __launch_bounds__(256) void fabrik_calc_any_kernel(int nj, const double *dists,
+                                                              const double *init, int shared,
+                                                              const double *goals, int64_t n,
+                                                              double tol2, int max_iter,
+                                                              double *joints, int32_t *iters,
+                                                              DevStats *S) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = i < n;
+  int it = 0;
+  if (valid) {
+    const double *ip = shared ? init : init + (size_t)i * nj * 3;
+    double *row = joints + (size_t)i * nj * 3;
+    auto ld = [&](const double *p, int k) -> d3 { return {p[3 * k], p[3 * k + 1], p[3 * k + 2]}; };
+    auto stj = [&](int k, d3 v) {
+      row[3 * k] = v.x;
+      row[3 * k + 1] = v.y;
+      row[3 * k + 2] = v.z;
+    };
+    for (int k = 0; k < nj; ++k) stj(k, ld(ip, k));
+    const d3 g = {goals[3 * i], goals[3 * i + 1], goals[3 * i + 2]};
+    const d3 start = ld(ip, 0);
+    double se = 1.0, ge = 1.0;
+    int st = IK_OK;
+    while (((se > tol2) || (ge > tol2)) && (max_iter > it)) {  // squared errors
+      d3 b = g;  // B[nj - 1]
+      stj(nj - 1, b);
+      for (int k = nj - 2; k >= 0; --k) {
+        b = point_between(b, ld(row, k), dists[k], st);
+        stj(k, b);
+      }
+      se = dist3_sq(b, start);  // B[0]
+      d3 f = start;
+      stj(0, f);
+      for (int k = 1; k < nj; ++k) {
+        f = point_between(f, ld(row, k), dists[k], st);
+        stj(k, f);
+      }
+      ge = dist3_sq(f, g);
+      ++it;
+      if (st != IK_OK) break;
+    }
+    if (st != IK_OK) record_error(S, i, st);
+    if (iters) iters[i] = it;
+  }
+  block_iter_stats(S, valid, it, max_iter);
+}
+
 void launch_fabrik_calc(int nj, const double *dists, const double *init, bool init_shared,
                         const double *goals, int64_t n, double tol, int max_iter,
                         double *joints, int32_t *iters, DevStats *S, hipStream_t st) {
@@ -1265,6 +1318,8 @@ void launch_fabrik_calc(int nj, const double *dists, const double *init, bool in
     IK_CALC_CASE(7)
     IK_CALC_CASE(8)
     default:
+      hipLaunchKernelGGL(fabrik_calc_any_kernel, dim3(grid), dim3(256), 0, st, nj, dists, init,
+                         sh, goals, n, tol2, max_iter, joints, iters, S);
       break;
   }
   kt_end(st);

@@ -104,6 +104,11 @@ struct ik_ctx {
   const void *ann_wh[ikhip::kAnnMaxLayers] = {};  // fp16x3 weight operand of each layer
   float ann_hinv[ikhip::kAnnMaxLayers] = {};      // fp16x3: 2^-(weight pre-scale exponent)
   int ann_mode = IK_ANN_FP32;
+  // a model outside the fused kernel's caps runs layer at a time (ik_ann_big.hip)
+  bool ann_big = false;
+  ikhip::AnnBigModel ann_bigm;  // its layers (pointers into ann_buf)
+  void *ann_act = nullptr;      // its activation buffers, grow-only
+  size_t ann_act_bytes = 0;
   int fabrik_variant = 1;
   int fabrik_bpc = 0;   // IKHIP_FABRIK_BPC: iteration-kernel blocks per CU (0 = size rule)
   int fabrik_core = 2;  // IKHIP_FABRIK_CORE: 2 core + reuse, 1 sqrt_core / div_core, 0 general

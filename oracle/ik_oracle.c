@@ -29,6 +29,7 @@
  */
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #define IKO_PI 3.141592653589793 /* math.pi */
@@ -199,13 +200,13 @@ void iko_fk(const double *dh, const double *ang, int64_t n, double *xyz, double 
 }
 
 /* ------------------------------------------------------------ FABRIK ---- */
-/* fabrik.py:44-67 for a chain of nj joints; returns iterations run. */
+/* fabrik.py:44-67 for a chain of nj (>= 1) joints; returns iterations run.
+ * B / F: nj points of caller-provided scratch each. */
 static int fabrik_calc(int nj, const double *dists, pt3 *cur, pt3 goal, double tol, int max_iter,
-                       int *st) {
+                       int *st, pt3 *B, pt3 *F) {
   pt3 start = cur[0];
   double se = 1.0, ge = 1.0;
   int step = 0;
-  pt3 B[16], F[16];
   while (((se > tol) || (ge > tol)) && (max_iter > step)) {
     /* __backward, fabrik.py:19-29 */
     B[nj - 1] = goal;
@@ -222,12 +223,17 @@ static int fabrik_calc(int nj, const double *dists, pt3 *cur, pt3 goal, double t
   return step;
 }
 
-/* Batch Fabrik.calculate with one init chain per point (init: n x nj x 3). */
-void iko_fabrik_calc(int nj, const double *dists, const double *init, const double *goals,
-                     int64_t n, double tol, int max_iter, double *out_joints, int32_t *iters,
-                     int32_t *status) {
+/* Batch Fabrik.calculate with one init chain per point (init: n x nj x 3), any
+ * nj >= 1 (fabrik.py takes any length with len(init) == len(dists)).  Returns 0,
+ * or -1 when nj < 1 or the scratch cannot be allocated. */
+int iko_fabrik_calc(int nj, const double *dists, const double *init, const double *goals,
+                    int64_t n, double tol, int max_iter, double *out_joints, int32_t *iters,
+                    int32_t *status) {
+  if (nj < 1) return -1;
+  pt3 *cur = (pt3 *)malloc(sizeof(pt3) * 3 * (size_t)nj);
+  if (!cur) return -1;
+  pt3 *B = cur + nj, *F = cur + 2 * nj;
   for (int64_t i = 0; i < n; ++i) {
-    pt3 cur[16];
     for (int k = 0; k < nj; ++k) {
       cur[k].x = init[(i * nj + k) * 3 + 0];
       cur[k].y = init[(i * nj + k) * 3 + 1];
@@ -235,7 +241,7 @@ void iko_fabrik_calc(int nj, const double *dists, const double *init, const doub
     }
     pt3 g = {goals[3 * i], goals[3 * i + 1], goals[3 * i + 2]};
     int st = IKO_OK;
-    int it = fabrik_calc(nj, dists, cur, g, tol, max_iter, &st);
+    int it = fabrik_calc(nj, dists, cur, g, tol, max_iter, &st, B, F);
     iters[i] = it;
     status[i] = st;
     for (int k = 0; k < nj; ++k) {
@@ -244,6 +250,8 @@ void iko_fabrik_calc(int nj, const double *dists, const double *init, const doub
       out_joints[(i * nj + k) * 3 + 2] = cur[k].z;
     }
   }
+  free(cur);
+  return 0;
 }
 
 /* inverse.py:54-112 */
@@ -300,7 +308,8 @@ void iko_fabrik_ikine(const double *dh, const double *links, const double *pts, 
     int st = fk_chain(dh, th, cur, 0);
     int it = 0;
     double a[4] = {NAN, NAN, NAN, NAN};
-    if (st == IKO_OK) it = fabrik_calc(4, links, cur, g, tol, max_iter, &st);
+    pt3 B[4], F[4];
+    if (st == IKO_OK) it = fabrik_calc(4, links, cur, g, tol, max_iter, &st, B, F);
     if (st == IKO_OK) get_angles(cur, a, &st);
     status[i] = st;
     iters[i] = it;

@@ -109,8 +109,9 @@ def fabrik_calc(init, goals, dists=LINKS, tol=1e-3, max_iter=100):
     g = np.ascontiguousarray(goals, dtype=np.float64).reshape(n, 3)
     d = np.ascontiguousarray(dists, dtype=np.float64)
     out = np.empty_like(init); it = np.empty(n, np.int32); st = np.empty(n, np.int32)
-    lib().iko_fabrik_calc(nj, _d(d), _d(init), _d(g), n, float(tol), int(max_iter), _d(out),
-                          _i(it), _i(st))
+    if lib().iko_fabrik_calc(nj, _d(d), _d(init), _d(g), n, float(tol), int(max_iter), _d(out),
+                             _i(it), _i(st)) != 0:
+        raise ValueError(f"iko_fabrik_calc: bad chain length {nj}")
     return out, it, st
 
 

@@ -175,6 +175,38 @@ def test_fabrik_calc_generic_chain(ctx1):
     assert np.abs(out - g["joints"]).max() <= 1e-9
 
 
+@pytest.mark.parametrize("nj", [1, 9, 13, 24])
+def test_fabrik_calc_any_length(ctx1, nj):
+    """fabrik_calc_any_kernel (chains outside the unrolled 2..8 joints) against the
+    reference's outputs (make_golden_chains.py) and the oracle: bit-exact iteration
+    counts and joints (same point_between sequence, same order)."""
+    g = _load("fabrik_calc_chains.npz")
+    links, init, goals = g[f"links_{nj}"], g[f"init_{nj}"], g[f"goals_{nj}"]
+    out, it, st = ctx1.fabrik_calc(links, init, goals, float(g["tol"]), int(g["max_iter"]))
+    assert st.first_err == -1
+    assert np.array_equal(it, g[f"iters_{nj}"])
+    assert np.array_equal(out, g[f"joints_{nj}"])
+    # one init chain shared by every goal (init_shared), against the oracle
+    out2, it2, _ = ctx1.fabrik_calc(links, init[0], goals, 1e-3, 60)
+    rout, rit, rst = O.fabrik_calc(np.broadcast_to(init[0], init.shape), goals, links, 1e-3, 60)
+    assert np.array_equal(it2, rit) and np.array_equal(out2, rout)
+
+
+def test_fabrik_calc_any_length_zero_division(ctx1):
+    """A zero-length segment raises ZeroDivisionError in the reference
+    (point.py:40-43): status IK_E_ZERODIV at the lowest failing goal."""
+    nj = 10
+    links = np.full(nj, 0.5)
+    init = np.zeros((nj, 3))
+    init[:, 2] = np.arange(nj) * 0.5
+    init[4] = init[3]  # coincident joints 3 and 4
+    goals = np.array([[0.2, 0.1, 2.0], [0.3, 0.2, 2.5], [0.1, 0.1, 1.5]])
+    _, _, st = ctx1.fabrik_calc(links, init, goals, 1e-3, 100)
+    _, _, rst = O.fabrik_calc(np.broadcast_to(init, (3, nj, 3)), goals, links, 1e-3, 100)
+    assert rst[0] == O.E_ZERODIV
+    assert st.first_err == 0 and st.first_err_code == 3
+
+
 def test_fabrik_calculate_dropin():
     """tests/fabrik_unit.py:17-41 through the GPU Fabrik class."""
     from inversekinematicsann_amd.kinematics.fabrik import Fabrik
@@ -243,6 +275,12 @@ def _ann_case(ctx, dims, acts_hidden, n, seed, check_limits=False, fk=False):
     ((3, 1024, 1024, 4), "tanh"),
     ((3, 768, 500, 4), "tanh"),
     ((3, 600, 1000, 37, 4), "relu"),
+    # past the fused kernel's caps (> 24 layers, or wider than 1024): the layered
+    # path (ik_ann_big.hip), activations through HBM
+    ((3, 2048, 2048, 4), "tanh"),
+    ((3,) + (64,) * 29 + (4,), "tanh"),         # 30 layers
+    ((3, 1100, 37, 4), "relu"),
+    ((3,) + (40,) * 25 + (4,), "sigmoid"),
 ])
 def test_ann_vs_oracle(ctx1, dims, act):
     n = 4099  # not a multiple of the 64-point tile
@@ -250,6 +288,28 @@ def test_ann_vs_oracle(ctx1, dims, act):
     assert ang.dtype == np.float32 and ang.shape == (n, 4)
     d = np.abs(ang.astype(np.float64) - ref64).max()
     assert d <= NS_TOL, d  # north_star: 1e-5 absolute
+
+
+def test_ann_layered_chunks_and_stats(ctx1, monkeypatch):
+    """The layered path over many chunks (a 1 MiB activation budget: 128-row
+    chunks of a 1100-wide model) equals one chunk bit for bit, and its limits
+    check and FK round-trip stats match the fused kernel's semantics."""
+    dims = (3, 1100, 4)
+    _, pts, ang1, err1, st1, ref64 = _ann_case(ctx1, dims, "tanh", 5000, seed=8,
+                                               check_limits=True, fk=True)
+    monkeypatch.setenv("IKHIP_ANN_ACT_MB", "1")
+    ang2, err2, st2 = ctx1.ann_solve(pts, check_limits=True, want_fk_err=True)
+    assert np.array_equal(ang1, ang2) and np.array_equal(err1, err2)
+    assert np.abs(ang2.astype(np.float64) - ref64).max() <= NS_TOL
+    assert st2.first_oob == st1.first_oob
+    assert st2.max_fk_err == err2.max()
+    assert abs(st2.sum_fk_err - err2.sum()) <= 1e-9 * err2.sum()
+    xyz, _, _ = ctx1.fk(ang2.astype(np.float64))
+    assert np.abs(err2 - np.sqrt(((xyz - pts) ** 2).sum(axis=1))).max() <= 1e-9
+    bad = pts.copy()
+    bad[77] = (0.0, 0.0, 50.0)
+    _, _, st3 = ctx1.ann_solve(bad, check_limits=True)
+    assert st3.first_oob == 77
 
 
 @pytest.mark.parametrize("hidden", [True, False])

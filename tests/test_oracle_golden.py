@@ -55,6 +55,18 @@ def test_oracle_fabrik_calc_generic_chain():
     assert np.array_equal(out, g["joints"])
 
 
+@pytest.mark.parametrize("nj", [1, 9, 13, 24])
+def test_oracle_fabrik_calc_any_length(nj):
+    """Chains outside 2..8 joints (make_golden_chains.py: the reference's own
+    outputs), bit-exact: fabrik.py:44-67 takes any len(init) == len(dists)."""
+    g = _load("fabrik_calc_chains.npz")
+    out, it, st = O.fabrik_calc(g[f"init_{nj}"], g[f"goals_{nj}"], g[f"links_{nj}"],
+                                float(g["tol"]), int(g["max_iter"]))
+    assert (st == 0).all()
+    assert np.array_equal(it, g[f"iters_{nj}"])
+    assert np.array_equal(out, g[f"joints_{nj}"])
+
+
 def test_oracle_round8():
     g = _load("round8.npz")
     r = np.array([O.round_nd(v, 8) for v in g["v"]])
