@@ -28,6 +28,7 @@ Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import math
 import json
 import os
@@ -526,7 +527,17 @@ def run_fabrik(job, args, tol=None, max_iter=None):
         solve(wpts, wang, wit, werr)
 
     ctx.fabrik_reset_order()  # start from a fresh context's table, whatever ran before
-    res = timed(ctx, step, args, world, warm=warm)
+    table = {}
+
+    def after_warm():
+        # the work-order table the timed steps start from: the same bytes in every
+        # process of the same build and batch (process spread)
+        t = ctx.fabrik_order_get()
+        table["sha16"] = hashlib.sha256(t.tobytes()).hexdigest()[:16]
+        table["cells_seen"] = int((t > 0).sum())
+
+    res = timed(ctx, step, args, world, warm=warm, after_warm=after_warm)
+    res["order_table"] = table
     del wpts, wang, wit, werr
     st = ctx.stats_fetch()
     if job.sc is not None:
@@ -636,7 +647,7 @@ def warm_batch(n):
     return random_dist(n, seed=2)
 
 
-def timed(ctx, step, args, world, warm=None):
+def timed(ctx, step, args, world, warm=None, after_warm=None):
     """W warm-up steps, one step timed per kernel, then K steps between barriers.
     Every wait on the steps is ctx.sync() first (ik_ctx_sync): bounded by the
     communicator's deadline at N > 1, so a stuck peer ends the run with
@@ -646,6 +657,8 @@ def timed(ctx, step, args, world, warm=None):
         (warm or step)()
     ctx.sync()
     torch.cuda.synchronize()
+    if after_warm is not None:
+        after_warm()
     # per-kernel HIP-event durations of one representative step
     ctx.set_timing(True)
     step()
@@ -950,7 +963,7 @@ def main():
                                 **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
                                                       "mean_iters", "n_capped", "end_to_end",
                                                       "gather_chunks", "gather_ms", "cold",
-                                                      "gather_check")
+                                                      "gather_check", "order_table")
                                    if k in r2}}
             cref = _config_ref("fabrik" if other.startswith("fabrik") else other, total, world,
                                1e-5 if other == "fabrik_tol1e-5" else args.tol,
@@ -991,7 +1004,7 @@ def main():
         "kernels_ms": res["kernels"],
     }
     for k in ("max_fk_err", "mean_fk_err", "p99_fk_err", "fk_err_note", "mean_iters", "n_capped",
-              "end_to_end", "gather_ms", "cold"):
+              "end_to_end", "gather_ms", "cold", "order_table"):
         if k in res:
             line[k] = res[k]
     if secondary:

@@ -82,9 +82,8 @@ def test_ann_without_model_and_bad_models():
         def dense(i, o):
             return rng.standard_normal((i, o)).astype(np.float32), np.zeros(o, np.float32)
 
-        # too wide (the wide build's LDS tile holds 1024 features), wrong input /
-        # output widths
-        for dims in ((3, 1100, 4), (4, 16, 4), (3, 16, 5)):
+        # wider than the layered path takes (16384), wrong input / output widths
+        for dims in ((3, 16385, 4), (4, 16, 4), (3, 16, 5)):
             ws, bs = zip(*[dense(dims[k], dims[k + 1]) for k in range(len(dims) - 1)])
             with pytest.raises(N.NativeError) as ei:
                 c.ann_load(list(ws), list(bs), ["tanh"] * (len(dims) - 2) + ["linear"], XS.mean,

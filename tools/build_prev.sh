@@ -15,7 +15,8 @@ done
 cd $T/a/csrc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $EXTRA"
 objs=""
-for o in ik_fk ik_fabrik ik_ann ik_ann_x ik_ann_w ik_shard; do
+for o in ik_fk ik_fabrik ik_ann ik_ann_x ik_ann_w ik_ann_big ik_shard; do
+  [ -f $o.hip ] || continue  # (ik_ann_big.hip: r04 on)
   /opt/rocm/bin/hipcc $FLAGS -c $o.hip -o $o.o & objs="$objs $o.o"
 done
 for o in ik_pipe ik_api; do
