@@ -727,6 +727,12 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 #ifndef IKHIP_ITER_WAVES
 #define IKHIP_ITER_WAVES 2
 #endif
+#ifndef IKHIP_FAB_REFILL_PRIO  // 1: the refill (park, stage, hand-out) at raised wave priority
+#define IKHIP_FAB_REFILL_PRIO 0
+#endif
+#ifndef IKHIP_FAB_PREP_CARRY  // 1 (CORE 2): the seed's carried quotient taken in the prepare step
+#define IKHIP_FAB_PREP_CARRY 0
+#endif
 constexpr int kIterWaves = IKHIP_ITER_WAVES;  // waves per SIMD = blocks per CU
 template <int REFILL_MIN, bool ORD, int CORE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kIterWaves, kIterWaves))) void
@@ -748,6 +754,10 @@ fabrik_iter_kernel(FabArgs a) {
   struct PrepBatch {
     double v[12][64];  // seed joints 0..2 and the goal
     long long idx[64];
+#if IKHIP_FAB_PREP_CARRY
+    double c[4][64];   // CORE 2: the seed's carry (cq, cd), taken at full width
+    uint32_t cdom[64];
+#endif
   };
   __shared__ PrepBatch batches[4];
   PrepBatch &PB = batches[threadIdx.x >> 6];
@@ -814,6 +824,7 @@ fabrik_iter_kernel(FabArgs a) {
     if (dry && nfree == 64) break;
     IKHIP_DG(kDiagLoops, 1);
     if (!dry && (nfree >= REFILL_MIN || nfree == 64)) {
+      if (IKHIP_FAB_REFILL_PRIO) prio_raise();
       IKHIP_DG(kDiagRefills, 1);
       IKHIP_DT(kDiagTRefill);  // refill time, less the flushes and preparations in it
       IKHIP_DT(kDiagTSub);
@@ -825,6 +836,7 @@ fabrik_iter_kernel(FabArgs a) {
           IKHIP_DG(kDiagFlushes, 1);
           IKHIP_DT(kDiagTEnd);  // (scratch slot: the flush's start)
           ring_flush<ORD>(a, R, rcnt, lane, acc);
+          if (IKHIP_FAB_REFILL_PRIO) prio_raise();  // (the flush dropped it)
           IKHIP_DT_ACC(kDiagFlushTicks, kDiagTEnd);
           IKHIP_DT_ACC(kDiagTRefill, kDiagTEnd);  // (not refill time)
           rcnt = 0;
@@ -907,8 +919,18 @@ fabrik_iter_kernel(FabArgs a) {
             PB.v[6][lane] = Js[2].x; PB.v[7][lane] = Js[2].y; PB.v[8][lane] = Js[2].z;
             PB.v[9][lane] = ng.x; PB.v[10][lane] = ng.y; PB.v[11][lane] = ng.z;
             PB.idx[lane] = ni;
+#if IKHIP_FAB_PREP_CARRY
+            if constexpr (CORE == 2) {
+              double pq;
+              d3 pd;
+              uint32_t pdom;
+              reuse_carry(Js[2], ng, L[3], pq, pd, pdom);
+              PB.c[0][lane] = pq; PB.c[1][lane] = pd.x; PB.c[2][lane] = pd.y; PB.c[3][lane] = pd.z;
+              PB.cdom[lane] = pdom;
+            }
+#endif
           }
-          prio_drop();
+          if (!IKHIP_FAB_REFILL_PRIO) prio_drop();
 #ifdef IKHIP_DIAG
           // (the seed's loads are consumed before the stamp)
           __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the batch's LDS writes landed
@@ -931,13 +953,22 @@ fabrik_iter_kernel(FabArgs a) {
           ge = 1.0;
           step = 0;
           active = true;
+#if IKHIP_FAB_PREP_CARRY
+          if constexpr (CORE == 2) {
+            cq = PB.c[0][src];
+            cd = {PB.c[1][src], PB.c[2][src], PB.c[3][src]};
+            cdom = PB.cdom[src];
+          }
+#else
           if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
+#endif
         }
         pptr += take;
         handed += take;
       }
       dry = nstage < 0 && pptr >= pcount;
       IKHIP_DT_ACC(kDiagRefillTicks, kDiagTRefill);
+      if (IKHIP_FAB_REFILL_PRIO) prio_drop();
     }
 #if IKHIP_FAB_INNER
     // iterate until a refill is due (REFILL_MIN lanes free) or, once the queue is

@@ -383,15 +383,17 @@ def test_ann_sigmoid_accuracy(ctx1, hidden):
 
 
 def test_ann_width_cap(ctx1):
-    """ik_ann_load takes widths up to 1024 and refuses only wider layers."""
+    """ik_ann_load takes widths up to 16384 (past 1024 through the layered path)
+    and refuses only wider layers."""
     from inversekinematicsann_amd import _native
     from inversekinematicsann_amd.kinematics.ann import glorot_model, REFERENCE_X_SCALER as XS, \
         REFERENCE_Y_SCALER as YS
-    m = glorot_model(dims=(3, 1025, 4), seed=1)
-    with pytest.raises(_native.NativeError, match="1..1024"):
+    m = glorot_model(dims=(3, 16385, 4), seed=1)
+    with pytest.raises(_native.NativeError, match="1..16384"):
         ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
-    m = glorot_model(dims=(3, 1024, 4), seed=1)
-    ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+    for w in (1024, 1025, 16384):
+        m = glorot_model(dims=(3, w, 4), seed=1)
+        ctx1.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
 
 
 @pytest.mark.parametrize("mode", ["bf16x6", "fp16x3"])
