@@ -1188,6 +1188,15 @@ constexpr int ann_waves() {
 #ifndef IKHIP_ANN_DYN  // 1: tiles claimed from a counter after the first; 0: static stride
 #define IKHIP_ANN_DYN 1
 #endif
+// Where the claim is issued.  0: by thread 0 at the tile's start (r02); its
+// returning atomic is older than wave 0's first weight loads, so vmcnt (counted
+// in issue order) makes wave 0's first weight wait of layer 0 wait for it too.
+// 1: by the workgroup's last wave after the tile's last GEMM, when that wave
+// has no memory wait left in the tile (point I/O is wave 0's), so the atomic's
+// latency hides under the output epilogue.
+#ifndef IKHIP_ANN_CLAIM
+#define IKHIP_ANN_CLAIM 0
+#endif
 template <int MR, int X>
 __global__ __launch_bounds__((64 * ann_waves<MR, X>()), (MR == 2 || kWide) ? 1 : 2) void
 ann_fused_kernel(AnnArgs a) {
@@ -1213,7 +1222,7 @@ ann_fused_kernel(AnnArgs a) {
   int64_t it_local = 0;  // this workgroup's tile counter
   for (int64_t tile = blockIdx.x; tile < ntiles; ++it_local) {
 #if IKHIP_ANN_DYN
-    if (tid == 0)
+    if (IKHIP_ANN_CLAIM == 0 && tid == 0)
       next_tile[it_local & 1] = (long long)atomicAdd(tile_ctr, 1ull) + (long long)gridDim.x;
 #endif
     const int64_t pt = tile * BM + tid;
@@ -1298,6 +1307,10 @@ ann_fused_kernel(AnnArgs a) {
       __syncthreads();
       stamp(sl ? sl + 1 : nullptr);
     }
+#if IKHIP_ANN_DYN
+    if (IKHIP_ANN_CLAIM == 1 && tid == W * 64 - 64)
+      next_tile[it_local & 1] = (long long)atomicAdd(tile_ctr, 1ull) + (long long)gridDim.x;
+#endif
     // ---- output: StandardScaler.inverse_transform (in-place fp32, fp64 ops) + FK
     if (tid < BM) {
       bool valid = pt < a.n;
