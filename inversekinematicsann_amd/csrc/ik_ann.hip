@@ -1188,14 +1188,17 @@ constexpr int ann_waves() {
 #ifndef IKHIP_ANN_DYN  // 1: tiles claimed from a counter after the first; 0: static stride
 #define IKHIP_ANN_DYN 1
 #endif
-// Where the claim is issued.  0: by thread 0 at the tile's start (r02); its
+// Where the claim is issued.  0: by thread 0 at the tile's start (r02-r03); its
 // returning atomic is older than wave 0's first weight loads, so vmcnt (counted
 // in issue order) makes wave 0's first weight wait of layer 0 wait for it too.
-// 1: by the workgroup's last wave after the tile's last GEMM, when that wave
+// 1 (r04): by the workgroup's last wave after the tile's last GEMM, when that wave
 // has no memory wait left in the tile (point I/O is wave 0's), so the atomic's
-// latency hides under the output epilogue.
+// latency hides under the output epilogue.  Same box, bit-identical: fp32
+// 39.44 -> 39.17 ms, HBM traffic 33.6 -> 23.2 GB per launch, L2 hit 80.7 -> 86.2 %
+// (the workgroups of an XCD stay closer in phase, sharing more weight lines);
+// fp16x3 even (profiles/r04/ab/ann_claim_late.txt).
 #ifndef IKHIP_ANN_CLAIM
-#define IKHIP_ANN_CLAIM 0
+#define IKHIP_ANN_CLAIM 1
 #endif
 template <int MR, int X>
 __global__ __launch_bounds__((64 * ann_waves<MR, X>()), (MR == 2 || kWide) ? 1 : 2) void

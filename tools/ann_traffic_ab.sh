@@ -9,7 +9,8 @@ export TMPDIR=/tmp
 OUT=gpurun_out/anntraffic
 mkdir -p $OUT
 BENCH="--method ann --secondary 0 --cpu-seconds 0 --end-to-end 0 --cold 0 --steps 5 --warmup 2"
-for lib in libikhip.so libikhip_dyn0.so; do
+LIBS=${LIBS:-"libikhip.so libikhip_dyn0.so"}
+for lib in $LIBS; do
   i=0
   for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"; do
     i=$((i+1))
@@ -21,5 +22,5 @@ for lib in libikhip.so libikhip_dyn0.so; do
     if [ $rc -ne 0 ]; then exit $rc; fi
   done
 done
-python tools/ann_traffic_summary.py --dir $OUT > $OUT/summary.txt 2>&1
+python tools/ann_traffic_summary.py --dir $OUT --builds $(echo $LIBS | sed "s/\.so//g") > $OUT/summary.txt 2>&1
 cat $OUT/summary.txt

@@ -22,8 +22,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dir", required=True)
     ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--builds", nargs="*", default=["libikhip", "libikhip_dyn0"])
     args = ap.parse_args()
-    for lib in ("libikhip", "libikhip_dyn0"):
+    for lib in args.builds:
         fig = {"build": lib}
         vals = {}
         ms_all = []
