@@ -485,6 +485,12 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
 #define IKHIP_ORD_PPT 16
 #endif
 constexpr int kOrdPPT = IKHIP_ORD_PPT;  // points per thread of the classify / scatter blocks
+// 1: classify and scatter in one launch (fabrik_classify_scatter_kernel): the queue
+// lives in kOrdClasses per-class regions of n entries (perm[k * n + slot]), so a
+// block needs no global class totals before it places its points (r04)
+#ifndef IKHIP_FAB_FUSED_SCATTER
+#define IKHIP_FAB_FUSED_SCATTER 1
+#endif
 
 // The shoulder (the seed's first joint, the translation of A_1) is
 // (a1 cos t1, a1 sin t1, d1) with t1 the goal's own azimuth: its distance from the
@@ -626,6 +632,71 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
   }
 }
 
+// 1'. classify + scatter in one pass (IKHIP_FAB_FUSED_SCATTER).  Each point's cell
+// and class as in classify; a wave ranks its points of one class with four
+// ballots (the lanes whose class bits all agree) and one LDS atomic per class
+// present (one lane per class: no same-address serialization); the block then
+// reserves a run in each class region with one global atomic per class and writes
+// its points there.  The sampled points' cells go straight into the high halves of
+// their cost-table sample words (the retire step fills in the low halves).
+__global__ __launch_bounds__(256) void fabrik_classify_scatter_kernel(FabArgs a) {
+  __shared__ unsigned int cnt[kOrdClasses], base[kOrdClasses];
+  __shared__ uint8_t cls[kOrdCells];
+  const int t = threadIdx.x, lane = t & 63;
+  const int64_t b0 = (int64_t)blockIdx.x * (256 * kOrdPPT);
+  d3 g[kOrdPPT];
+#pragma unroll
+  for (int j = 0; j < kOrdPPT; ++j) {  // all loads in flight before the first use
+    const int64_t i = b0 + j * 256 + t;
+    if (i < a.n) g[j] = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
+  }
+  if (t < kOrdClasses) cnt[t] = 0;
+  static_assert(kOrdCells % 256 == 0, "whole table rows per thread");
+  unsigned int key[kOrdCells / 256];
+#pragma unroll
+  for (int q = 0; q < kOrdCells / 256; ++q) key[q] = a.ord->key[t + 256 * q];
+#pragma unroll
+  for (int q = 0; q < kOrdCells / 256; ++q)
+    cls[t + 256 * q] = (uint8_t)key_class(key[q], a.max_iter);
+  __syncthreads();
+  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  unsigned int loc[kOrdPPT];
+  int kk[kOrdPPT];
+#pragma unroll
+  for (int j = 0; j < kOrdPPT; ++j) {
+    const int64_t i = b0 + j * 256 + t;
+    const bool valid = i < a.n;
+    int k = 0;
+    if (valid) {
+      const int cell = goal_cell(a.r, g[j]);
+      k = cls[cell];
+      if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
+        reinterpret_cast<uint16_t *>(&a.ord->sample[i / kOrdSample])[1] = (uint16_t)cell;
+    }
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 4; ++bit) {
+      const bool on = (k >> bit) & 1;
+      const unsigned long long b = __ballot(on);
+      peers &= on ? b : ~b;
+    }
+    const int leader = __ffsll((long long)peers) - 1;
+    unsigned int r0 = 0;
+    if (valid && lane == leader) r0 = atomicAdd(&cnt[k], (unsigned int)__popcll(peers));
+    r0 = __shfl(r0, leader < 0 ? lane : leader, 64);
+    loc[j] = r0 + (unsigned int)__popcll(peers & lt);
+    kk[j] = k;
+  }
+  __syncthreads();
+  if (t < kOrdClasses) base[t] = cnt[t] ? atomicAdd(&a.S->cls_cur[t][0], cnt[t]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kOrdPPT; ++j) {
+    const int64_t i = b0 + j * 256 + t;
+    if (i < a.n) a.perm[(int64_t)kk[j] * a.n + base[kk[j]] + loc[j]] = (int32_t)i;
+  }
+}
+
 // 3. persistent iteration with per-lane refill, seed and angles in batches.
 //
 // A lane whose point converged is refilled from the wave's batch of prepared
@@ -703,9 +774,13 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
     const int it = R.it[lane];
     commit_point(a, i, J, {R.g[0][lane], R.g[1][lane], R.g[2][lane]}, it, st, th, acc);
     if constexpr (ORD) {
-      if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
-        a.ord->sample[i / kOrdSample] = ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) |
-                                        (uint32_t)(it < 0xffff ? it : 0xffff);
+      if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample) {
+        const uint32_t lo = (uint32_t)(it < 0xffff ? it : 0xffff);
+        if (IKHIP_FAB_FUSED_SCATTER)  // (the cell is already in the high half)
+          reinterpret_cast<uint16_t *>(&a.ord->sample[i / kOrdSample])[0] = (uint16_t)lo;
+        else
+          a.ord->sample[i / kOrdSample] = ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) | lo;
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -771,6 +846,10 @@ fabrik_iter_kernel(FabArgs a) {
   // until that one runs dry; then the next one its block has not seen dry)
   __shared__ unsigned int dry_heads;  // the heads this block found dry
   if (threadIdx.x == 0) dry_heads = 0;
+  // IKHIP_FAB_FUSED_SCATTER: the class regions' fill, hardest class first
+  __shared__ unsigned int ctot[kOrdClasses];
+  if (IKHIP_FAB_FUSED_SCATTER && ORD && threadIdx.x < kOrdClasses)
+    ctot[threadIdx.x] = a.S->cls_cur[kOrdClasses - 1 - threadIdx.x][0];
   __syncthreads();
   int head = (int)(blockIdx.x % kQueueHeads);
   unsigned long long na = 0;
@@ -875,7 +954,25 @@ fabrik_iter_kernel(FabArgs a) {
           return;
         }
         ncount = (int)min((int64_t)a.chunk, a.n - nbase);
-        if (lane < ncount) nperm = ORD ? (int64_t)a.perm[nbase + lane] : nbase + lane;
+        if (lane < ncount) {
+          if (!ORD) {
+            nperm = nbase + lane;
+          } else if (IKHIP_FAB_FUSED_SCATTER) {
+            // queue position -> (class region, slot), hardest class first
+            int64_t q = nbase + lane;
+            int k = 0;
+#pragma unroll
+            for (int c = 0; c < kOrdClasses - 1; ++c) {
+              const int64_t tc = ctot[c];
+              const bool past = k == c && q >= tc;
+              q -= past ? tc : 0;
+              k += past ? 1 : 0;
+            }
+            nperm = (int64_t)a.perm[(int64_t)(kOrdClasses - 1 - k) * a.n + q];
+          } else {
+            nperm = (int64_t)a.perm[nbase + lane];
+          }
+        }
         nstage = 2;
       };
       auto stage3 = [&]() {
@@ -1093,7 +1190,8 @@ __global__ __launch_bounds__(256) void fabrik_fold_kernel(FabArgs a) {
 static size_t up256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t fabrik_scratch_bytes(int64_t n) {
-  // work order: perm n int32, cell n uint16
+  // work order: perm n int32 (fused: kOrdClasses regions of n), cell n uint16 (unfused)
+  if (IKHIP_FAB_FUSED_SCATTER) return up256((size_t)n * 4 * kOrdClasses) + 1024;
   return up256((size_t)n * 4) + up256((size_t)n * 2) + 1024;
 }
 
@@ -1170,16 +1268,22 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   const bool ordered = ord && order_on && n < (int64_t)1 << 31;
   if (ordered) {
     char *p = static_cast<char *>(scratch);
-    a.perm = reinterpret_cast<int32_t *>(p);
-    p += up256((size_t)n * 4);
-    a.cell = reinterpret_cast<uint16_t *>(p);
     const unsigned ogrid = (unsigned)((n + 256 * kOrdPPT - 1) / (256 * kOrdPPT));
-    kt_begin("fabrik_classify_kernel", stream);
-    hipLaunchKernelGGL(fabrik_classify_kernel, dim3(ogrid), dim3(256), 0, stream, a);
-    kt_end(stream);
-    kt_begin("fabrik_scatter_kernel", stream);
-    hipLaunchKernelGGL(fabrik_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
-    kt_end(stream);
+    a.perm = reinterpret_cast<int32_t *>(p);
+    if (IKHIP_FAB_FUSED_SCATTER) {
+      kt_begin("fabrik_classify_scatter_kernel", stream);
+      hipLaunchKernelGGL(fabrik_classify_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
+      kt_end(stream);
+    } else {
+      p += up256((size_t)n * 4);
+      a.cell = reinterpret_cast<uint16_t *>(p);
+      kt_begin("fabrik_classify_kernel", stream);
+      hipLaunchKernelGGL(fabrik_classify_kernel, dim3(ogrid), dim3(256), 0, stream, a);
+      kt_end(stream);
+      kt_begin("fabrik_scatter_kernel", stream);
+      hipLaunchKernelGGL(fabrik_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
+      kt_end(stream);
+    }
   }
   // persistent grid: blocks_per_cu 256-thread blocks per CU (= waves per SIMD)
   // measured on MI355X (tools/sweep_fabrik.py): at 1M points 2 blocks/CU with

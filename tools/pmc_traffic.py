@@ -21,12 +21,14 @@ import json
 import os
 from collections import defaultdict
 
-KERNELS = ("ann_fused_kernel", "fabrik_iter_kernel", "fabrik_classify_kernel",
+KERNELS = ("ann_fused_kernel", "fabrik_iter_kernel", "fabrik_classify_scatter_kernel",
+           "fabrik_classify_kernel",
            "fabrik_scatter_kernel", "fabrik_fold_kernel", "fabrik_simple_kernel", "reset_stats_kernel",
            "gather_unpack_kernel", "fk_kernel")
 # every kernel one FABRIK solve launches (ik_fabrik.hip): the pipeline's bytes
-FABRIK_PIPELINE = ("reset_stats_kernel", "fabrik_classify_kernel", "fabrik_scatter_kernel",
-                   "fabrik_iter_kernel", "fabrik_fold_kernel")
+FABRIK_PIPELINE = ("reset_stats_kernel", "fabrik_classify_scatter_kernel",
+                   "fabrik_classify_kernel", "fabrik_scatter_kernel", "fabrik_iter_kernel",
+                   "fabrik_fold_kernel")
 
 
 def _short(name: str) -> str | None:

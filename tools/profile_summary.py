@@ -40,6 +40,7 @@ ORDER = ["ann", "fabrik", "fabrik_tol1e-5", "ann_bf16x6", "ann_fp16x3", "fk"]
 METHODS_OF = {"ann_fused_kernel": ["ann"],
               "ann_fused_kernel_bf16x6": ["ann_bf16x6"],
               "ann_fused_kernel_fp16x3": ["ann_fp16x3"],
+              "fabrik_classify_scatter_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fabrik_classify_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fabrik_scatter_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fabrik_iter_kernel": ["fabrik", "fabrik_tol1e-5"],
@@ -159,10 +160,11 @@ def main():
                     1.0, avg["SQ_LDS_IDX_ACTIVE"])
             r["counters"] = avg
     for m in ("fabrik", "fabrik_tol1e-5"):
+        # the build's own pipeline: fused classify + scatter (r04) or the two kernels
         ks = [k for k in FABRIK_PIPELINE if k in res[m]]
-        if len(ks) == len(FABRIK_PIPELINE):
+        if "fabrik_iter_kernel" in ks and "reset_stats_kernel" in ks:
             res[m]["fabrik_pipeline"] = {
-                "kernels": list(FABRIK_PIPELINE),
+                "kernels": ks,
                 "rocprof_avg_ms": sum(res[m][k]["rocprof_avg_ms"] for k in ks),
                 "hbm_bytes_per_launch": sum(res[m][k].get("hbm_bytes_per_launch", 0.0) for k in ks),
                 "hbm_bytes_per_launch_raw": sum(res[m][k].get("hbm_bytes_per_launch_raw", 0.0)
