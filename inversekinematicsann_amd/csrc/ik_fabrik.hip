@@ -487,9 +487,13 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
 constexpr int kOrdPPT = IKHIP_ORD_PPT;  // points per thread of the classify / scatter blocks
 // 1: classify and scatter in one launch (fabrik_classify_scatter_kernel): the queue
 // lives in kOrdClasses per-class regions of n entries (perm[k * n + slot]), so a
-// block needs no global class totals before it places its points (r04)
+// block needs no global class totals before it places its points.  r04, rocprof over
+// the timed windows, same box (profiles/r04/ab/fabrik_fused_scatter.txt): the one
+// launch takes 17.8 us against 13.5 + 9.8, but its queue order inside a cost class
+// (block-major, ballot ranks) makes the iteration kernel 4 % slower at tol 1e-3
+// (0.340 against 0.327 ms; even at 1e-5), with the same learned table: off.
 #ifndef IKHIP_FAB_FUSED_SCATTER
-#define IKHIP_FAB_FUSED_SCATTER 1
+#define IKHIP_FAB_FUSED_SCATTER 0
 #endif
 
 // The shoulder (the seed's first joint, the translation of A_1) is
@@ -802,8 +806,12 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 #ifndef IKHIP_ITER_WAVES
 #define IKHIP_ITER_WAVES 2
 #endif
-#ifndef IKHIP_FAB_REFILL_PRIO  // 1: the refill (park, stage, hand-out) at raised wave priority
-#define IKHIP_FAB_REFILL_PRIO 0
+// 1: the refill (park, stage, hand-out) at raised wave priority, like the seed and
+// angles steps: its dependent chains issue when ready instead of in the partner's
+// leftover slots.  r04, same box: iteration kernel -1.7 % at tol 1e-3, -1.3 % at 1e-5
+// (rocprof windows, 3 / 2 runs each), -1.0 / -1.3 % per bench step in another lease.
+#ifndef IKHIP_FAB_REFILL_PRIO
+#define IKHIP_FAB_REFILL_PRIO 1
 #endif
 #ifndef IKHIP_FAB_PREP_CARRY  // 1 (CORE 2): the seed's carried quotient taken in the prepare step
 #define IKHIP_FAB_PREP_CARRY 0
