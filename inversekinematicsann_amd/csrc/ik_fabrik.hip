@@ -495,11 +495,9 @@ constexpr int kOrdPPT = IKHIP_ORD_PPT;  // points per thread of the classify / s
 #ifndef IKHIP_FAB_FUSED_SCATTER
 #define IKHIP_FAB_FUSED_SCATTER 0
 #endif
-// 1: the scatter spreads each block's run of a class over its slots (a grab's points
-// then come from the whole 4096-point block instead of a few rows of it)
-#ifndef IKHIP_FAB_SPREAD
-#define IKHIP_FAB_SPREAD 0
-#endif
+// (r04: spreading a block's class run over its slots -- slot r * 4099 mod run length --
+// so that a grab's points come from the whole block: iteration kernel +0.9 %, scatter
+// +3 us; profiles/r04/ab/fabrik_order_spread_dropped.txt)
 
 // The shoulder (the seed's first joint, the translation of A_1) is
 // (a1 cos t1, a1 sin t1, d1) with t1 the goal's own azimuth: its distance from the
@@ -632,25 +630,6 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
     base[t] = start + (cnt[t] ? atomicAdd(&a.S->cls_cur[t][sh], cnt[t]) : 0u);
   }
   __syncthreads();
-#if IKHIP_FAB_SPREAD
-  // the block's run of class c spread over its slots: slot r * P mod cnt[c] (P = 4099,
-  // a prime above any run length, so the map is a permutation of the run)
-  __shared__ unsigned int run0[kOrdClasses], rk[kOrdClasses];
-  if (t < kOrdClasses) {
-    run0[t] = base[t];
-    rk[t] = 0;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kOrdPPT; ++j) {
-    if (cl[j] != 0xffff) {
-      const int c = cl[j] >> 10;
-      const unsigned int r = atomicAdd(&rk[c], 1u);
-      const unsigned int pos = run0[c] + (unsigned int)(((unsigned long long)r * 4099u) % cnt[c]);
-      a.perm[pos] = (int32_t)(b0 + j * 256 + t);
-    }
-  }
-#else
 #pragma unroll
   for (int j = 0; j < kOrdPPT; ++j) {
     if (cl[j] != 0xffff) {
@@ -658,7 +637,6 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
       a.perm[pos] = (int32_t)(b0 + j * 256 + t);
     }
   }
-#endif
 }
 
 // 1'. classify + scatter in one pass (IKHIP_FAB_FUSED_SCATTER).  Each point's cell
