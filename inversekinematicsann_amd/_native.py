@@ -550,9 +550,9 @@ class Context:
 
     def kernel_times(self):
         """[(kernel name, ms)] of the last call (after set_timing(True))."""
-        ms = np.zeros(16, np.float32)
-        names = ctypes.create_string_buffer(16 * 48)
-        n = self.lib.ik_kernel_times(self.handle, 16, ms.ctypes.data, ctypes.addressof(names), 48)
+        ms = np.zeros(64, np.float32)
+        names = ctypes.create_string_buffer(64 * 48)
+        n = self.lib.ik_kernel_times(self.handle, 64, ms.ctypes.data, ctypes.addressof(names), 48)
         if n < 0:
             raise NativeError(-n, self.lib.ik_last_error().decode())
         raw = names.raw

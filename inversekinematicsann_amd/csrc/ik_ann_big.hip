@@ -86,8 +86,17 @@ __global__ __launch_bounds__(256) void annb_gemm_kernel(const float *__restrict_
   __shared__ __attribute__((aligned(16))) float As[2][kBM * kLdA];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t row0 = (int64_t)blockIdx.x * kBM;
-  const int nt0 = blockIdx.y * (kBN / 32) + wn * 2;  // this wave's two column tiles
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
+  // workgroup b runs on XCD b % 8; XCD x takes row panels x, x + 8, ... and every
+  // column block of a panel in turn, so a panel's A tile is read from HBM once into
+  // that XCD's L2 and reused by all its column blocks
+  const int nCB = (NT + kBN / 32 - 1) / (kBN / 32);
+  const unsigned b = blockIdx.x, xcd = b & 7u, k = b >> 3;
+  const int64_t rb = (int64_t)(k / (unsigned)nCB) * 8 + xcd;
+  const int cb = (int)(k % (unsigned)nCB);
+  if (rb * kBM >= rows) return;  // the grid's last panel row is padded to 8
+  const int64_t row0 = rb * kBM;
+  const int nt0 = cb * (kBN / 32) + wn * 2;  // this wave's two column tiles
   const int r = lane & 31, h = lane >> 5;
   f32x16 acc[2][2];
 #pragma unroll
@@ -95,22 +104,25 @@ __global__ __launch_bounds__(256) void annb_gemm_kernel(const float *__restrict_
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[m][j] = (f32x16)(0.0f);
 
-  // the A tile of one stage: 128 rows x 32 floats, 4 x 16 bytes per thread
+  // the A tile of one stage: 128 rows x 32 floats, 4 x 16 bytes per thread, loaded
+  // two stages ahead into one of two register sets (the loads' HBM latency under
+  // load outlasts one stage of MFMAs) and written to the LDS buffer of its stage at
+  // the end of the stage before
   const int nst = (G + 3) / 4;
-  f32x4 ra[4];
-  auto load_a = [&](int s) {
+  f32x4 ra0[4], ra1[4];
+  auto load_a = [&](f32x4 (&ra)[4], int s) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + 256 * i;
       const int row = idx >> 3, c4 = idx & 7;
       const int64_t gr = row0 + row;
       const int kk = s * kBK + 4 * c4;
-      ra[i] = (gr < rows && kk < lda)
+      ra[i] = (s < nst && gr < rows && kk < lda)
                   ? *reinterpret_cast<const f32x4 *>(A + gr * (int64_t)lda + kk)
                   : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
   };
-  auto store_a = [&](int buf) {
+  auto store_a = [&](const f32x4 (&ra)[4], int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + 256 * i;
@@ -118,14 +130,9 @@ __global__ __launch_bounds__(256) void annb_gemm_kernel(const float *__restrict_
       *reinterpret_cast<f32x4 *>(&As[buf][row * kLdA + 4 * c4]) = ra[i];
     }
   };
-  load_a(0);
-  store_a(0);
-  __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
-    if (s + 1 < nst) load_a(s + 1);
-    // the stage's weight fragments (zero for column tiles past the layer)
-    f32x4 b[4][2];
+  // the weight fragments of stage s (zero for column tiles past the layer), loaded one
+  // stage ahead so that their L2 latency hides under the stage before's MFMAs
+  auto load_b = [&](f32x4 (&b)[4][2], int s) {
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
@@ -134,6 +141,18 @@ __global__ __launch_bounds__(256) void annb_gemm_kernel(const float *__restrict_
         b[u][j] = (g < G && nt < NT) ? wp[((size_t)nt * G + g) * 64 + lane]
                                      : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       }
+  };
+  // stage s: the next stage's weights and the A tile two ahead go out, the MFMAs of
+  // this stage run, then the A tile of stage s + 1 (loaded one stage ago) goes to LDS
+  auto stage = [&](int s, f32x4 (&bn)[4][2], f32x4 (&ra_fill)[4], const f32x4 (&ra_next)[4]) {
+    const int buf = s & 1;
+    f32x4 b[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[u][j] = bn[u][j];
+    if (s + 1 < nst) load_b(bn, s + 1);
+    if (s + 2 < nst) load_a(ra_fill, s + 2);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if (s * 4 + u >= G) break;
@@ -150,8 +169,19 @@ __global__ __launch_bounds__(256) void annb_gemm_kernel(const float *__restrict_
           for (int m = 0; m < 2; ++m)
             acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][q], b[u][j][q], acc[m][j], 0, 0, 0);
     }
-    if (s + 1 < nst) store_a(buf ^ 1);
+    if (s + 1 < nst) store_a(ra_next, buf ^ 1);
     __syncthreads();
+  };
+  f32x4 bn[4][2];
+  load_b(bn, 0);
+  load_a(ra0, 0);
+  load_a(ra1, 1);
+  store_a(ra0, 0);
+  __syncthreads();
+  // even stages fill ra0 (stage s + 2) and store ra1 (stage s + 1); odd ones the reverse
+  for (int s = 0; s < nst; s += 2) {
+    stage(s, bn, ra0, ra1);
+    if (s + 1 < nst) stage(s + 1, bn, ra1, ra0);
   }
   // bias (after the dot product, as Keras adds it) + activation, stored per
   // accumulator element: lane (r, h) holds column r of rows (q&3) + 8(q>>2) + 4h
@@ -247,7 +277,8 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
     int cur = 0, lda = 8;
     for (const AnnBigLayer &L : m.layers) {
       const int G = L.kp / 8, NT = L.np / 32;
-      const dim3 grid((unsigned)((rows + kBM - 1) / kBM), (unsigned)((NT + 3) / 4));
+      const int64_t nRB = (rows + kBM - 1) / kBM;
+      const dim3 grid((unsigned)((nRB + 7) / 8 * 8 * ((NT + 3) / 4)));
       kt_begin("annb_gemm_kernel", st);
       hipLaunchKernelGGL(annb_gemm_kernel, grid, dim3(256), 0, st, buf[cur], lda, rows,
                          reinterpret_cast<const f32x4 *>(L.wp), G, NT, L.bias, L.act,

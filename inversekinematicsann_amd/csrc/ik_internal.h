@@ -12,7 +12,7 @@
 #include "ik_common.h"
 
 namespace ikhip {
-constexpr int kMaxTimed = 16;
+constexpr int kMaxTimed = 64;  // kernels timed per call (the layered ANN path launches one per layer)
 struct KTimer {
   bool on = false;
   int n = 0;
