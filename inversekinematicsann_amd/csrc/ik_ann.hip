@@ -723,6 +723,40 @@ struct WStepH16 {
   f16x8 p[NR][2][2];  // [tile][feature half][plane]
 };
 
+// IKHIP_ANN_PREFETCH (fp16x3 on 16x16x32, layers of 16 column tiles): a layer's
+// epilogue loads the next layer's bias and first weight step into registers as it
+// frees the accumulators of each column tile, so the next layer's first MFMAs do not
+// wait for them after the barrier (the r03 stamps: a layer's first K step ends
+// ~4.7 k cycles after the layer before, for ~1.6 k of MFMAs).
+#ifndef IKHIP_ANN_PREFETCH
+#define IKHIP_ANN_PREFETCH 0
+#endif
+struct PreH16 {
+  WStepH16<4> w;       // the next layer's first weight step (4 column tiles per wave)
+  f32x4 b[4][2];       // ... and its bias
+  bool have = false;   // w / b hold this layer's
+  bool want = false;   // this layer's epilogue loads the next layer's
+  const void *nwx = nullptr;
+  int nxbytes = 0, nG32 = 0;
+  const float *nbias = nullptr;
+  // w / b are dead once consumed (or when a layer skips the prefetch): poison them,
+  // so the registers are not carried -- and spilled -- through the layers between
+  __device__ __forceinline__ void drop_regs() {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int fh = 0; fh < 2; ++fh) {
+        b[j][fh] = __builtin_nondeterministic_value(b[j][fh]);
+#pragma unroll
+        for (int p = 0; p < 2; ++p) w.p[j][fh][p] = __builtin_nondeterministic_value(w.p[j][fh][p]);
+      }
+  }
+  __device__ __forceinline__ void drop() {
+    have = false;
+    drop_regs();
+  }
+};
+
 template <int NR>
 __device__ __forceinline__ void load_wh16(WStepH16<NR> &w, const WStream<NR> &ws, int g) {
 #pragma unroll
@@ -790,28 +824,43 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
     for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
 }
 
-template <int MR, int NR, int W = kWaves>
+template <int MR, int NR, int W = kWaves, bool PF = false>
 __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__restrict__ wx,
                                                int G32, int xbytes, float xinv, int wave, int lane,
                                                const float *bias, f32x16 (&acc)[MR][NR],
-                                               unsigned long long *st_first = nullptr) {
+                                               unsigned long long *st_first = nullptr,
+                                               PreH16 *pre = nullptr) {
   const _Float16 *ap = hplane(const_cast<float *>(H), lane & 15) + 8 * (lane >> 4);
   // the bias loads go out before the first weight step's: vmcnt counts in issue
   // order, so the accumulators' start (bias x scale) then waits for the bias
   // alone and the first MFMAs for their own weight blocks, not for all of the
   // step's (IKHIP_ANN_BIAS_FIRST)
   f32x4 bl[NR][2];
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int fh = 0; fh < 2; ++fh)
-      bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
-                                                   4 * (lane >> 4));
-  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
-  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
   WStepH16<NR> w[kH16Ring];
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
+  bool pref = false;
+  if constexpr (PF) pref = pre->have;
+  if constexpr (PF) {
+    if (pref) {  // the layer before loaded them during its epilogue
 #pragma unroll
-  for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
+      for (int j = 0; j < NR; ++j)
+#pragma unroll
+        for (int fh = 0; fh < 2; ++fh) bl[j][fh] = pre->b[j][fh];
+      w[0] = pre->w;
+    }
+    pre->drop_regs();
+  }
+  if (!pref) {
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int fh = 0; fh < 2; ++fh)
+        bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
+                                                     4 * (lane >> 4));
+    if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
+  }
   f32x4 c4[MR][NR][4];
   const float scale = 1.0f / xinv;  // exact: xinv is 2^-k
 #pragma unroll
@@ -853,14 +902,16 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
 // Epilogue of an fp16x3 layer in the 16x16 sub-tile layout above: per lane and
 // sub-tile four consecutive features of one point, one 8-byte store per plane
 // (or one ds_write_b128 of fp32).
-template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
+template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves, bool PF = false>
 __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
                                                 f32x16 (&acc)[MR][NR], unsigned long long *st,
-                                                float pre = 1.0f) {
+                                                float pre = 1.0f, PreH16 *pf = nullptr) {
   stamp(st);
   __syncthreads();  // every wave has finished reading the layer input
+  bool want = false;
+  if constexpr (PF) want = pf->want;
 #pragma unroll
-  for (int j = 0; j < NR; ++j)
+  for (int j = 0; j < NR; ++j) {
 #pragma unroll
     for (int fh = 0; fh < 2; ++fh) {
       const int col = (wave + W * j) * 32 + 16 * fh + 4 * (lane >> 4);
@@ -882,6 +933,20 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
         }
       }
     }
+    if constexpr (PF) {
+      if (want) {  // column tile j's accumulators are free: its share of the next layer
+        const WStream<4> wsn = make_wstream<4>(pf->nwx, pf->nxbytes, wave, W, pf->nG32 * 4, lane);
+#pragma unroll
+        for (int fh = 0; fh < 2; ++fh) {
+          pf->b[j][fh] = *reinterpret_cast<const f32x4 *>(pf->nbias + (wave + W * j) * 32 +
+                                                          16 * fh + 4 * (lane >> 4));
+#pragma unroll
+          for (int p = 0; p < 2; ++p) pf->w.p[j][fh][p] = wload<f16x8>(wsn, j, fh * 2 + p);
+        }
+      }
+    }
+  }
+  if constexpr (PF) pf->have = want;
 }
 
 // bf16x6 on v_mfma_f32_16x16x32_bf16 (IKHIP_ANN_X16): the same six products in
@@ -1036,13 +1101,13 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
 // a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
 // layer is one) stores the activations as split planes.
-template <int ACT, bool HOUT, int W, int X, int MR, int NR>
+template <int ACT, bool HOUT, int W, int X, bool PF, int MR, int NR>
 __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[NR], int wave,
                                           int lane, f32x16 (&acc)[MR][NR],
-                                          unsigned long long *st, float pre) {
+                                          unsigned long long *st, float pre, PreH16 *pf) {
   if (tr) {
     if constexpr ((X == 2 && kH16) || (X == 1 && kX16))
-      layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st, pre);
+      layer_store_h16<MR, NR, ACT, HOUT, W, PF>(H, wave, lane, acc, st, pre, pf);
     else layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
   } else {
     layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
@@ -1051,24 +1116,26 @@ __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[N
 
 // pre: the fp16x3 16x16x32 GEMM's accumulators still carry the weight pre-scale
 // (layer_gemm_h16); 1 for every other layer.
-template <bool HOUT, int W, int X, int MR, int NR>
+template <bool HOUT, int W, int X, bool PF = false, int MR, int NR>
 __device__ __forceinline__ void store_act(int act, bool tr, float *H, const float (&bv)[NR],
                                           int wave, int lane, f32x16 (&acc)[MR][NR],
-                                          unsigned long long *st, float pre = 1.0f) {
+                                          unsigned long long *st, float pre = 1.0f,
+                                          PreH16 *pf = nullptr) {
   switch (act) {
-    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
-    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
-    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
-    default: store_any<IK_ACT_LINEAR, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
+    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
+    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
+    default: store_any<IK_ACT_LINEAR, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
   }
 }
 
-template <int MR, int NR, int X = 0, bool HX = false, int W = kWaves>
+template <int MR, int NR, int X = 0, bool HX = false, int W = kWaves, bool PF = false>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           unsigned long long *st_first,
                                           const void *wx = nullptr, int G16 = 0,
-                                          float xinv = 1.0f, bool hout = false) {
+                                          float xinv = 1.0f, bool hout = false,
+                                          PreH16 *pf = nullptr) {
   f32x16 acc[MR][NR];
   const int NT = wbytes / (G * 1024);  // column tiles of the layer
   float bv[NR];
@@ -1083,8 +1150,8 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
                                 wave, lane, bias, acc);
     }
     else if constexpr (kH16)  // G16: 32-deep K steps here
-      layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
-                                xinv, wave, lane, bias, acc, st_first);
+      layer_gemm_h16<MR, NR, W, PF>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
+                                xinv, wave, lane, bias, acc, st_first, pf);
     else
       layer_gemm_h<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024,
                               xinv, wave, lane, bias, acc);
@@ -1094,8 +1161,8 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
     layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, W, lane, nullptr, acc, st_first);
   }
   const float pre = (X == 2 && kH16 && tr) ? xinv : 1.0f;
-  if (HX && hout) store_act<true, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
-  else store_act<false, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
+  if (HX && hout) store_act<true, W, X, PF>(act, tr, H, bv, wave, lane, acc, st, pre, pf);
+  else store_act<false, W, X, PF>(act, tr, H, bv, wave, lane, acc, st, pre, pf);
 }
 
 // HOUT: the next layer runs fp16x3, so the result goes out as split planes
@@ -1256,6 +1323,7 @@ ann_fused_kernel(AnnArgs a) {
     __syncthreads();
     stamp(stp ? stp + 1 : nullptr);
     // ---- Dense layers
+    PreH16 pf;  // IKHIP_ANN_PREFETCH: the next layer's first weight step
     for (int l = 0; l < a.m.n_layers; ++l) {
       const int G = a.m.kp[l] >> 3;
       const int NT = a.m.np[l] >> 5;
@@ -1270,15 +1338,30 @@ ann_fused_kernel(AnnArgs a) {
                         (a.m.np[l + 1] >> 5) > 1;
       if (NT == 1) {
         run_layer_splitk<MR, X == 2, W>(H, wp, bias, act, G, wave, lane, tid, sl, hout);
+        pf.drop();
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
         // K steps of the split GEMM: 16 deep (bf16x6, 32x32x16 fp16x3), 32 (16x16x32)
         const int G16 =
             ((X == 2 && kH16) || (X == 1 && kX16)) ? (a.m.kp[l] + 31) >> 5 : (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
+        bool pref_ok = false;
+        if constexpr (X == 2 && kH16 && IKHIP_ANN_PREFETCH && W * 4 <= 16) {
+          // the next layer takes the same path with 4 column tiles on every wave
+          const int ln = l + 1;
+          pref_ok = cnt == 4 && ln < a.m.n_layers && a.m.wx[ln] != nullptr &&
+                    (a.m.np[ln] >> 5) == 4 * W;
+          pf.want = pref_ok;
+          if (pref_ok) {
+            pf.nwx = a.m.wx[ln];
+            pf.nG32 = (a.m.kp[ln] + 31) >> 5;
+            pf.nxbytes = (a.m.np[ln] >> 5) * pf.nG32 * 4 * 1024;
+            pf.nbias = a.m.bias[ln];
+          }
+        }
         switch (cnt) {
           case 4:
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W, X == 2 && kH16 && IKHIP_ANN_PREFETCH>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout, &pf);
             break;
           case 3:
             if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
@@ -1287,7 +1370,9 @@ ann_fused_kernel(AnnArgs a) {
           case 1: run_layer<MR, 1, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
           default: __syncthreads(); break;
         }
+        if (cnt != 4) pf.drop();
       } else {
+        pf.drop();
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
