@@ -731,6 +731,12 @@ struct WStepH16 {
 #ifndef IKHIP_ANN_PREFETCH
 #define IKHIP_ANN_PREFETCH 0
 #endif
+#ifndef IKHIP_ANN_PREFETCH_LATE  // 1: after the last column tile's epilogue
+#define IKHIP_ANN_PREFETCH_LATE 0
+#endif
+#ifndef IKHIP_ANN_PREFETCH_BIAS  // 0: the bias still loads at the layer start
+#define IKHIP_ANN_PREFETCH_BIAS 0
+#endif
 struct PreH16 {
   WStepH16<4> w;       // the next layer's first weight step (4 column tiles per wave)
   f32x4 b[4][2];       // ... and its bias
@@ -845,7 +851,11 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
 #pragma unroll
       for (int j = 0; j < NR; ++j)
 #pragma unroll
-        for (int fh = 0; fh < 2; ++fh) bl[j][fh] = pre->b[j][fh];
+        for (int fh = 0; fh < 2; ++fh)
+          bl[j][fh] = IKHIP_ANN_PREFETCH_BIAS
+                          ? pre->b[j][fh]
+                          : *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 +
+                                                             16 * fh + 4 * (lane >> 4));
       w[0] = pre->w;
     }
     pre->drop_regs();
@@ -934,14 +944,17 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
       }
     }
     if constexpr (PF) {
-      if (want) {  // column tile j's accumulators are free: its share of the next layer
+      if (want && (!IKHIP_ANN_PREFETCH_LATE || j == NR - 1)) {  // column tile j's accumulators are free: its share of the next layer
         const WStream<4> wsn = make_wstream<4>(pf->nwx, pf->nxbytes, wave, W, pf->nG32 * 4, lane);
 #pragma unroll
-        for (int fh = 0; fh < 2; ++fh) {
-          pf->b[j][fh] = *reinterpret_cast<const f32x4 *>(pf->nbias + (wave + W * j) * 32 +
-                                                          16 * fh + 4 * (lane >> 4));
+        for (int jj = IKHIP_ANN_PREFETCH_LATE ? 0 : j; jj <= j; ++jj)
 #pragma unroll
-          for (int p = 0; p < 2; ++p) pf->w.p[j][fh][p] = wload<f16x8>(wsn, j, fh * 2 + p);
+        for (int fh = 0; fh < 2; ++fh) {
+          if (IKHIP_ANN_PREFETCH_BIAS)
+            pf->b[jj][fh] = *reinterpret_cast<const f32x4 *>(pf->nbias + (wave + W * jj) * 32 +
+                                                             16 * fh + 4 * (lane >> 4));
+#pragma unroll
+          for (int p = 0; p < 2; ++p) pf->w.p[jj][fh][p] = wload<f16x8>(wsn, jj, fh * 2 + p);
         }
       }
     }
@@ -1275,7 +1288,13 @@ ann_fused_kernel(AnnArgs a) {
   // + kHPad: the fp32 GEMM's operand ring reads up to 3 K groups past a row's end
   __shared__ __attribute__((aligned(16))) float H[BM * kLd + kHPad];
   const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
+#ifndef IKHIP_ANN_UNIFORM_WAVE
+#define IKHIP_ANN_UNIFORM_WAVE 0
+#endif
+  // wave index in an SGPR: the per-wave column-tile count (cnt) and the paths it
+  // selects are then uniform branches, not exec-masked regions
+  const int wave = IKHIP_ANN_UNIFORM_WAVE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+  const int lane = tid & 63;
   const int64_t ntiles = (a.n + BM - 1) / BM;
   double blk_max = 0.0, blk_sum = 0.0;  // FK round-trip error of this lane's points
 
@@ -1325,6 +1344,15 @@ ann_fused_kernel(AnnArgs a) {
     // ---- Dense layers
     PreH16 pf;  // IKHIP_ANN_PREFETCH: the next layer's first weight step
     for (int l = 0; l < a.m.n_layers; ++l) {
+#ifndef IKHIP_ANN_LAUNDER
+#define IKHIP_ANN_LAUNDER 0
+#endif
+      // an opaque (always 0) uniform offset on the LDS tile per layer: the layer
+      // functions' per-lane LDS addresses are then recomputed per layer instead of
+      // being hoisted out of the tile loop and held in registers across it
+      int hz = 0;
+      if (IKHIP_ANN_LAUNDER) asm volatile("" : "+s"(hz));
+      float *const HL = H + hz;
       const int G = a.m.kp[l] >> 3;
       const int NT = a.m.np[l] >> 5;
       const f32x4 *wp = reinterpret_cast<const f32x4 *>(a.m.wp[l]);
@@ -1337,7 +1365,7 @@ ann_fused_kernel(AnnArgs a) {
       const bool hout = X == 2 && l + 1 < a.m.n_layers && a.m.wx[l + 1] &&
                         (a.m.np[l + 1] >> 5) > 1;
       if (NT == 1) {
-        run_layer_splitk<MR, X == 2, W>(H, wp, bias, act, G, wave, lane, tid, sl, hout);
+        run_layer_splitk<MR, X == 2, W>(HL, wp, bias, act, G, wave, lane, tid, sl, hout);
         pf.drop();
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
@@ -1361,13 +1389,13 @@ ann_fused_kernel(AnnArgs a) {
         }
         switch (cnt) {
           case 4:
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W, X == 2 && kH16 && IKHIP_ANN_PREFETCH>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout, &pf);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W, X == 2 && kH16 && IKHIP_ANN_PREFETCH>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout, &pf);
             break;
           case 3:
-            if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
+            if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
             break;
-          case 2: run_layer<MR, 2, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
-          case 1: run_layer<MR, 1, X, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 2: run_layer<MR, 2, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 1: run_layer<MR, 1, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
           default: __syncthreads(); break;
         }
         if (cnt != 4) pf.drop();
@@ -1376,18 +1404,18 @@ ann_fused_kernel(AnnArgs a) {
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
             break;
           case 3:
-            if constexpr (W * 3 <= 16) run_layer<MR, 3, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
+            if constexpr (W * 3 <= 16) run_layer<MR, 3, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
             break;
-          case 2: run_layer<MR, 2, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
-          case 1: run_layer<MR, 1, 0, X == 2, W>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 2: run_layer<MR, 2, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 1: run_layer<MR, 1, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
 #ifdef IKHIP_ANN_WIDE
-          case 8: run_layer<MR, 8>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
-          case 7: run_layer<MR, 7>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
-          case 6: run_layer<MR, 6>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
-          case 5: run_layer<MR, 5>(H, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 8: run_layer<MR, 8>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 7: run_layer<MR, 7>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 6: run_layer<MR, 6>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
+          case 5: run_layer<MR, 5>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
 #endif
           default: __syncthreads(); break;  // idle wave still joins the barrier
         }
