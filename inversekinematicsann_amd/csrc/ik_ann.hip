@@ -319,19 +319,35 @@ __device__ __forceinline__ _Float16 *hplane(float *H, int row) {
   return reinterpret_cast<_Float16 *>(H + row * kLd);
 }
 
+// Plane swizzle (IKHIP_ANN_HSWZ): rows 4..11 of every 16 hold their 16-byte k-blocks
+// pairwise swapped (half index col ^ 8).  The 16x16x32 loop's ds_read_b128 of a K step
+// (lane: row lane & 15, k-block lane >> 4; kLd = 516 floats puts row r one 16-byte slot
+// after row r - 1) then lands each of the instruction's four 16-lane bank groups on 16
+// distinct slots; unswizzled, every group has one 2-way collision (rows 11 and 12 of
+// consecutive k-blocks), i.e. 8 LDS cycles instead of 4 (SQ_LDS_BANK_CONFLICT = 47 % of
+// SQ_LDS_IDX_ACTIVE in the r04 fp16x3 profile).  Writers (store_h4 / store_h1) and
+// readers apply the same XOR; it touches only bit 3 of the half index, so K-step and
+// row-group offsets (multiples of 16 halves / 16 rows) pass through unchanged.
+#ifndef IKHIP_ANN_HSWZ
+#define IKHIP_ANN_HSWZ 1
+#endif
+__device__ __forceinline__ int hswz(int row) {
+  return IKHIP_ANN_HSWZ ? (((row + 4) >> 3) & 1) << 3 : 0;
+}
+
 __device__ __forceinline__ void store_h4(float *H, int row, int col, f32x4 v) {
   const f32x2 v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
   const f16x2 h01 = __builtin_convertvector(v01, f16x2), h23 = __builtin_convertvector(v23, f16x2);
   const f16x2 l01 = __builtin_convertvector(v01 - __builtin_convertvector(h01, f32x2), f16x2);
   const f16x2 l23 = __builtin_convertvector(v23 - __builtin_convertvector(h23, f32x2), f16x2);
-  _Float16 *p = hplane(H, row) + col;
+  _Float16 *p = hplane(H, row) + (col ^ hswz(row));
   *reinterpret_cast<f16x4 *>(p) = f16x4{h01[0], h01[1], h23[0], h23[1]};
   *reinterpret_cast<f16x4 *>(p + 512) = f16x4{l01[0], l01[1], l23[0], l23[1]};
 }
 
 __device__ __forceinline__ void store_h1(float *H, int row, int col, float v) {
   const _Float16 h = (_Float16)v;
-  _Float16 *p = hplane(H, row) + col;
+  _Float16 *p = hplane(H, row) + (col ^ hswz(row));
   p[0] = h;
   p[512] = (_Float16)(v - (float)h);
 }
@@ -658,7 +674,7 @@ __device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__rest
                                              int G16, int xbytes, float xinv, int wave, int lane,
                                              const float *bias, f32x16 (&acc)[MR][NR]) {
   const int r = lane & 31, h = lane >> 5;
-  const _Float16 *ap = hplane(const_cast<float *>(H), r) + 8 * h;  // the split planes
+  const _Float16 *ap = hplane(const_cast<float *>(H), r) + ((8 * h) ^ hswz(r));  // the split planes
   acc_init_bias(acc, bias, wave, W, lane, 1.0f / xinv);  // exact: xinv is 2^-k
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G16 * 2, lane);
   WStepH<NR> w[kXRing];
@@ -836,7 +852,8 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
                                                const float *bias, f32x16 (&acc)[MR][NR],
                                                unsigned long long *st_first = nullptr,
                                                PreH16 *pre = nullptr) {
-  const _Float16 *ap = hplane(const_cast<float *>(H), lane & 15) + 8 * (lane >> 4);
+  const _Float16 *ap =
+      hplane(const_cast<float *>(H), lane & 15) + ((8 * (lane >> 4)) ^ hswz(lane & 15));
   // the bias loads go out before the first weight step's: vmcnt counts in issue
   // order, so the accumulators' start (bias x scale) then waits for the bias
   // alone and the first MFMAs for their own weight blocks, not for all of the
@@ -960,6 +977,212 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
     }
   }
   if constexpr (PF) pf->have = want;
+}
+
+// ---- IKHIP_ANN_SPLIT_EPI: the epilogue's transcendentals under the next MFMAs ----
+// A full-width fp16x3 layer (4 column tiles per wave, >= 16 K steps, tanh / sigmoid)
+// runs as P K passes of 4 / P column tiles each.  The activation of pass p - 1 (scale,
+// exp, rcp, fma, in place on its accumulators) is computed between the MFMAs of pass
+// p, one (row group, tile, feature half) chunk every few K steps, so that only the
+// last pass's activations remain after the layer's MFMAs (one wave per SIMD: the
+// epilogue otherwise leaves the SIMD's matrix core idle, 6.7 k cycles per layer in the
+// r03 stamps).  All passes store after the layer's barrier, as before; the same
+// operations on the same values, so the results are bit-identical.  Cost: the A
+// fragments are read from LDS once per pass.
+#ifndef IKHIP_ANN_SPLIT_EPI
+#define IKHIP_ANN_SPLIT_EPI 0  // 0: off; 2 or 4: passes
+#endif
+constexpr int kSplitSteps = 16;  // K steps unrolled per pass after the first
+static_assert(kSplitSteps % kH16Ring == 0, "the unrolled steps keep the ring's phase");
+static_assert(!(IKHIP_ANN_SPLIT_EPI && IKHIP_ANN_PREFETCH), "one layer-start scheme at a time");
+
+// chunk (m, j, fh) of a pass's accumulators: the activation in place (layer_store_h16's
+// pairs and order)
+template <int ACT, bool PIN = false, int MR, int NRP>
+__device__ __forceinline__ void epi_chunk(f32x4 (&c4)[MR][NRP][4], int m, int j, int fh,
+                                          float pre) {
+  f32x4 &a = c4[m][j][2 * fh];
+  f32x4 &b = c4[m][j][2 * fh + 1];
+  f32x2 t[4] = {f32x2{a.x, a.y}, f32x2{a.z, a.w}, f32x2{b.x, b.y}, f32x2{b.z, b.w}};
+  act_apply2x4<ACT>(t, pre);
+  a = f32x4{t[0].x, t[0].y, t[1].x, t[1].y};
+  b = f32x4{t[2].x, t[2].y, t[3].x, t[3].y};
+  // pinned here: left alone, the compiler sinks the chunk to its store after the barrier
+  if constexpr (PIN) asm volatile("" : "+v"(a), "+v"(b));
+}
+
+template <bool HOUT, int MR, int NRP>
+__device__ __forceinline__ void epi_put(float *H, const f32x4 (&c4)[MR][NRP][4], int nt0, int W,
+                                        int lane, int m, int j, int fh) {
+  const int col = (nt0 + W * j) * 32 + 16 * fh + 4 * (lane >> 4);
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {
+    const int row = m * 32 + 16 * ph + (lane & 15);
+    const f32x4 v = c4[m][j][2 * fh + ph];
+    if constexpr (HOUT) store_h4(H, row, col, v);
+    else *reinterpret_cast<f32x4 *>(H + row * kLd + col) = v;
+  }
+}
+
+// step_h16 with side work (a callable emitting VALU / transcendental instructions)
+// placed between the step's MFMAs: per pair of MFMAs one weight load and one LDS read
+// while they last, and up to two side instructions.
+template <int MR, int NR, int GI, typename Side>
+__device__ __forceinline__ void step_h16s(Split2 (&sa)[MR][2], const WStepH16<NR> &w,
+                                          WStepH16<NR> &fill, const WStream<NR> &ws,
+                                          const _Float16 *ab, int g, f32x4 (&acc)[MR][NR][4],
+                                          Side &&side) {
+  __builtin_amdgcn_sched_barrier(0);
+  load_wh16(fill, ws, g + kH16Ring - 1);
+  Split2 sn[MR][2];
+  load_ah16(sn, ab, GI + 1);
+  side();
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int j = 0; j < NR; ++j)
+#pragma unroll
+      for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+        for (int ph = 0; ph < 2; ++ph) {
+          f32x4 c = acc[m][j][2 * fh + ph];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].lo, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][1], sa[m][ph].hi, c, 0, 0, 0);
+          acc[m][j][2 * fh + ph] =
+              __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].hi, c, 0, 0, 0);
+        }
+#pragma unroll
+  for (int i = 0; i < 6 * MR * NR; ++i) {
+    if (i < 4 * NR) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
+    if (i < 4 * MR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+    __builtin_amdgcn_sched_group_barrier(0x402, 2, 0);                  // VALU / TRANS
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int m = 0; m < MR; ++m)
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
+}
+
+// One K pass over NR column tiles nt0 + W j (layer_gemm_h16's loop; the first GS steps
+// unrolled, with side(step) between their MFMAs).  c4 comes back pre-scaled as there.
+template <int MR, int NR, int W, int GS, typename Side>
+__device__ __forceinline__ void h16_pass(const _Float16 *ap, const f16x8 *__restrict__ wx, int G32,
+                                         int xbytes, float xinv, int nt0, int lane,
+                                         const float *bias, f32x4 (&c4)[MR][NR][4], Side &&side) {
+  f32x4 bl[NR][2];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh)
+      bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (nt0 + W * j) * 32 + 16 * fh +
+                                                   4 * (lane >> 4));
+  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
+  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, nt0, W, G32 * 4, lane);
+  WStepH16<NR> w[kH16Ring];
+#pragma unroll
+  for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
+  const float scale = 1.0f / xinv;  // exact: xinv is 2^-k
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh) {
+      const f32x4 b = bl[j][fh] * scale;
+#pragma unroll
+      for (int m = 0; m < MR; ++m) c4[m][j][2 * fh] = c4[m][j][2 * fh + 1] = b;
+    }
+  Split2 sa[MR][2];
+  load_ah16(sa, ap, 0);
+  int g = 0;
+  if constexpr (GS > 0) {
+    static_for<GS>([&](auto s) {
+      constexpr int u = s.value % kH16Ring;
+      step_h16s<MR, NR, u>(sa, w[u], w[(u + kH16Ring - 1) % kH16Ring], ws,
+                           ap + 32 * (s.value - u), s.value, c4, [&] { side(s); });
+    });
+    g = GS;
+  }
+  for (; g + kH16Ring <= G32; g += kH16Ring) {
+    const _Float16 *ab = ap + 32 * g;
+    static_for<kH16Ring>([&](auto u) {
+      step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
+                                g + u.value, c4);
+    });
+  }
+  const _Float16 *ab = ap + 32 * g;
+  static_for<kH16Ring - 1>([&](auto u) {
+    if (g + u.value < G32)
+      step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
+                                g + u.value, c4);
+  });
+}
+
+// The layer (G32 >= kSplitSteps): P passes, then the barrier, the stores of the passes
+// already activated, and the last pass's epilogue.
+template <int MR, int P, int ACT, bool HOUT, int W>
+__device__ __forceinline__ void layer_h16_split(float *H, const f16x8 *__restrict__ wx, int G32,
+                                                int xbytes, float xinv, int wave, int lane,
+                                                const float *bias, unsigned long long *st) {
+  constexpr int NRP = 4 / P;
+  constexpr int C = MR * NRP * 2;  // chunks per pass
+  constexpr int every = kSplitSteps / C;
+  static_assert(kSplitSteps % C == 0, "chunks spread evenly over the unrolled steps");
+  const _Float16 *ap =
+      hplane(H, lane & 15) + ((8 * (lane >> 4)) ^ hswz(lane & 15));
+  f32x4 c4[P][MR][NRP][4];
+  static_for<P>([&](auto p) {
+    constexpr int pv = p.value;
+    if constexpr (pv == 0) {
+      h16_pass<MR, NRP, W, 0>(ap, wx, G32, xbytes, xinv, wave, lane, bias, c4[0], [](auto) {});
+    } else {
+      h16_pass<MR, NRP, W, kSplitSteps>(
+          ap, wx, G32, xbytes, xinv, wave + W * NRP * pv, lane, bias, c4[pv], [&](auto s) {
+            if constexpr (s.value % every == 0) {
+              constexpr int c = s.value / every;
+              epi_chunk<ACT, true>(c4[pv - 1], c / (NRP * 2), (c >> 1) % NRP, c & 1, xinv);
+            }
+          });
+    }
+  });
+  stamp(st);
+  __syncthreads();  // every wave has finished reading the layer input
+  static_for<P - 1>([&](auto p) {
+#pragma unroll
+    for (int j = 0; j < NRP; ++j)
+#pragma unroll
+      for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+        for (int m = 0; m < MR; ++m)
+          epi_put<HOUT>(H, c4[p.value], wave + W * NRP * p.value, W, lane, m, j, fh);
+  });
+#pragma unroll
+  for (int j = 0; j < NRP; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh)
+#pragma unroll
+      for (int m = 0; m < MR; ++m) {
+        epi_chunk<ACT>(c4[P - 1], m, j, fh, xinv);
+        epi_put<HOUT>(H, c4[P - 1], wave + W * NRP * (P - 1), W, lane, m, j, fh);
+      }
+}
+
+template <int MR, int W>
+__device__ __forceinline__ void run_layer_h16_split(float *H, const void *wx, int G32, int NT,
+                                                    float xinv, int wave, int lane,
+                                                    const float *bias, int act, bool hout,
+                                                    unsigned long long *st) {
+  constexpr int P = IKHIP_ANN_SPLIT_EPI ? IKHIP_ANN_SPLIT_EPI : 2;
+  const f16x8 *w = static_cast<const f16x8 *>(wx);
+  const int xb = NT * G32 * 4 * 1024;
+  if (act == IK_ACT_TANH) {
+    if (hout) layer_h16_split<MR, P, IK_ACT_TANH, true, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
+    else layer_h16_split<MR, P, IK_ACT_TANH, false, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
+  } else {
+    if (hout) layer_h16_split<MR, P, IK_ACT_SIGMOID, true, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
+    else layer_h16_split<MR, P, IK_ACT_SIGMOID, false, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
+  }
 }
 
 // bf16x6 on v_mfma_f32_16x16x32_bf16 (IKHIP_ANN_X16): the same six products in
@@ -1289,7 +1512,7 @@ ann_fused_kernel(AnnArgs a) {
   __shared__ __attribute__((aligned(16))) float H[BM * kLd + kHPad];
   const int tid = threadIdx.x;
 #ifndef IKHIP_ANN_UNIFORM_WAVE
-#define IKHIP_ANN_UNIFORM_WAVE 0
+#define IKHIP_ANN_UNIFORM_WAVE 1
 #endif
   // wave index in an SGPR: the per-wave column-tile count (cnt) and the paths it
   // selects are then uniform branches, not exec-masked regions
@@ -1345,7 +1568,7 @@ ann_fused_kernel(AnnArgs a) {
     PreH16 pf;  // IKHIP_ANN_PREFETCH: the next layer's first weight step
     for (int l = 0; l < a.m.n_layers; ++l) {
 #ifndef IKHIP_ANN_LAUNDER
-#define IKHIP_ANN_LAUNDER 0
+#define IKHIP_ANN_LAUNDER 1
 #endif
       // an opaque (always 0) uniform offset on the LDS tile per layer: the layer
       // functions' per-lane LDS addresses are then recomputed per layer instead of
@@ -1389,6 +1612,12 @@ ann_fused_kernel(AnnArgs a) {
         }
         switch (cnt) {
           case 4:
+            if constexpr (X == 2 && kH16 && IKHIP_ANN_SPLIT_EPI && W * 4 <= 16) {
+              if (G16 >= kSplitSteps && (act == IK_ACT_TANH || act == IK_ACT_SIGMOID)) {
+                run_layer_h16_split<MR, W>(HL, wx, G16, NT, xinv, wave, lane, bias, act, hout, sl);
+                break;
+              }
+            }
             if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W, X == 2 && kH16 && IKHIP_ANN_PREFETCH>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout, &pf);
             break;
           case 3:

@@ -8,10 +8,16 @@ trap 'rm -rf $T' EXIT
 mkdir -p $T/a/csrc $T/include
 REV=${REV:-HEAD}
 OUT=${OUT:-libikhip_prev.so}
-git -C "$ROOT" show $REV:include/ikhip.h > $T/include/ikhip.h
-for f in $(git -C "$ROOT" ls-tree --name-only $REV inversekinematicsann_amd/csrc/); do
-  git -C "$ROOT" show $REV:$f > $T/a/csrc/$(basename $f)
-done
+if [ "$REV" = WORKTREE ]; then  # the working tree's sources (variant builds: EXTRA=-D...)
+  cp "$ROOT/include/ikhip.h" $T/include/
+  cp "$ROOT"/inversekinematicsann_amd/csrc/*.hip "$ROOT"/inversekinematicsann_amd/csrc/*.h \
+     "$ROOT"/inversekinematicsann_amd/csrc/*.cpp $T/a/csrc/
+else
+  git -C "$ROOT" show $REV:include/ikhip.h > $T/include/ikhip.h
+  for f in $(git -C "$ROOT" ls-tree --name-only $REV inversekinematicsann_amd/csrc/); do
+    git -C "$ROOT" show $REV:$f > $T/a/csrc/$(basename $f)
+  done
+fi
 cd $T/a/csrc
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off $EXTRA"
 objs=""
