@@ -739,46 +739,6 @@ struct WStepH16 {
   f16x8 p[NR][2][2];  // [tile][feature half][plane]
 };
 
-// IKHIP_ANN_PREFETCH (fp16x3 on 16x16x32, layers of 16 column tiles): a layer's
-// epilogue loads the next layer's bias and first weight step into registers as it
-// frees the accumulators of each column tile, so the next layer's first MFMAs do not
-// wait for them after the barrier (the r03 stamps: a layer's first K step ends
-// ~4.7 k cycles after the layer before, for ~1.6 k of MFMAs).
-#ifndef IKHIP_ANN_PREFETCH
-#define IKHIP_ANN_PREFETCH 0
-#endif
-#ifndef IKHIP_ANN_PREFETCH_LATE  // 1: after the last column tile's epilogue
-#define IKHIP_ANN_PREFETCH_LATE 0
-#endif
-#ifndef IKHIP_ANN_PREFETCH_BIAS  // 0: the bias still loads at the layer start
-#define IKHIP_ANN_PREFETCH_BIAS 0
-#endif
-struct PreH16 {
-  WStepH16<4> w;       // the next layer's first weight step (4 column tiles per wave)
-  f32x4 b[4][2];       // ... and its bias
-  bool have = false;   // w / b hold this layer's
-  bool want = false;   // this layer's epilogue loads the next layer's
-  const void *nwx = nullptr;
-  int nxbytes = 0, nG32 = 0;
-  const float *nbias = nullptr;
-  // w / b are dead once consumed (or when a layer skips the prefetch): poison them,
-  // so the registers are not carried -- and spilled -- through the layers between
-  __device__ __forceinline__ void drop_regs() {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int fh = 0; fh < 2; ++fh) {
-        b[j][fh] = __builtin_nondeterministic_value(b[j][fh]);
-#pragma unroll
-        for (int p = 0; p < 2; ++p) w.p[j][fh][p] = __builtin_nondeterministic_value(w.p[j][fh][p]);
-      }
-  }
-  __device__ __forceinline__ void drop() {
-    have = false;
-    drop_regs();
-  }
-};
-
 template <int NR>
 __device__ __forceinline__ void load_wh16(WStepH16<NR> &w, const WStream<NR> &ws, int g) {
 #pragma unroll
@@ -846,12 +806,11 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
     for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
 }
 
-template <int MR, int NR, int W = kWaves, bool PF = false>
+template <int MR, int NR, int W = kWaves>
 __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__restrict__ wx,
                                                int G32, int xbytes, float xinv, int wave, int lane,
                                                const float *bias, f32x16 (&acc)[MR][NR],
-                                               unsigned long long *st_first = nullptr,
-                                               PreH16 *pre = nullptr) {
+                                               unsigned long long *st_first = nullptr) {
   const _Float16 *ap =
       hplane(const_cast<float *>(H), lane & 15) + ((8 * (lane >> 4)) ^ hswz(lane & 15));
   // the bias loads go out before the first weight step's: vmcnt counts in issue
@@ -859,35 +818,17 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
   // alone and the first MFMAs for their own weight blocks, not for all of the
   // step's (IKHIP_ANN_BIAS_FIRST)
   f32x4 bl[NR][2];
-  WStepH16<NR> w[kH16Ring];
+#pragma unroll
+  for (int j = 0; j < NR; ++j)
+#pragma unroll
+    for (int fh = 0; fh < 2; ++fh)
+      bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
+                                                   4 * (lane >> 4));
+  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
-  bool pref = false;
-  if constexpr (PF) pref = pre->have;
-  if constexpr (PF) {
-    if (pref) {  // the layer before loaded them during its epilogue
+  WStepH16<NR> w[kH16Ring];
 #pragma unroll
-      for (int j = 0; j < NR; ++j)
-#pragma unroll
-        for (int fh = 0; fh < 2; ++fh)
-          bl[j][fh] = IKHIP_ANN_PREFETCH_BIAS
-                          ? pre->b[j][fh]
-                          : *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 +
-                                                             16 * fh + 4 * (lane >> 4));
-      w[0] = pre->w;
-    }
-    pre->drop_regs();
-  }
-  if (!pref) {
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-#pragma unroll
-      for (int fh = 0; fh < 2; ++fh)
-        bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
-                                                     4 * (lane >> 4));
-    if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
-  }
+  for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
   f32x4 c4[MR][NR][4];
   const float scale = 1.0f / xinv;  // exact: xinv is 2^-k
 #pragma unroll
@@ -929,16 +870,14 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
 // Epilogue of an fp16x3 layer in the 16x16 sub-tile layout above: per lane and
 // sub-tile four consecutive features of one point, one 8-byte store per plane
 // (or one ds_write_b128 of fp32).
-template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves, bool PF = false>
+template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
 __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
                                                 f32x16 (&acc)[MR][NR], unsigned long long *st,
-                                                float pre = 1.0f, PreH16 *pf = nullptr) {
+                                                float pre = 1.0f) {
   stamp(st);
   __syncthreads();  // every wave has finished reading the layer input
-  bool want = false;
-  if constexpr (PF) want = pf->want;
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
+  for (int j = 0; j < NR; ++j)
 #pragma unroll
     for (int fh = 0; fh < 2; ++fh) {
       const int col = (wave + W * j) * 32 + 16 * fh + 4 * (lane >> 4);
@@ -960,229 +899,6 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
         }
       }
     }
-    if constexpr (PF) {
-      if (want && (!IKHIP_ANN_PREFETCH_LATE || j == NR - 1)) {  // column tile j's accumulators are free: its share of the next layer
-        const WStream<4> wsn = make_wstream<4>(pf->nwx, pf->nxbytes, wave, W, pf->nG32 * 4, lane);
-#pragma unroll
-        for (int jj = IKHIP_ANN_PREFETCH_LATE ? 0 : j; jj <= j; ++jj)
-#pragma unroll
-        for (int fh = 0; fh < 2; ++fh) {
-          if (IKHIP_ANN_PREFETCH_BIAS)
-            pf->b[jj][fh] = *reinterpret_cast<const f32x4 *>(pf->nbias + (wave + W * jj) * 32 +
-                                                             16 * fh + 4 * (lane >> 4));
-#pragma unroll
-          for (int p = 0; p < 2; ++p) pf->w.p[jj][fh][p] = wload<f16x8>(wsn, jj, fh * 2 + p);
-        }
-      }
-    }
-  }
-  if constexpr (PF) pf->have = want;
-}
-
-// ---- IKHIP_ANN_SPLIT_EPI: the epilogue's transcendentals under the next MFMAs ----
-// A full-width fp16x3 layer (4 column tiles per wave, >= 16 K steps, tanh / sigmoid)
-// runs as P K passes of 4 / P column tiles each.  The activation of pass p - 1 (scale,
-// exp, rcp, fma, in place on its accumulators) is computed between the MFMAs of pass
-// p, one (row group, tile, feature half) chunk every few K steps, so that only the
-// last pass's activations remain after the layer's MFMAs (one wave per SIMD: the
-// epilogue otherwise leaves the SIMD's matrix core idle, 6.7 k cycles per layer in the
-// r03 stamps).  All passes store after the layer's barrier, as before; the same
-// operations on the same values, so the results are bit-identical.  Cost: the A
-// fragments are read from LDS once per pass.
-#ifndef IKHIP_ANN_SPLIT_EPI
-#define IKHIP_ANN_SPLIT_EPI 0  // 0: off; 2 or 4: passes
-#endif
-constexpr int kSplitSteps = 16;  // K steps unrolled per pass after the first
-static_assert(kSplitSteps % kH16Ring == 0, "the unrolled steps keep the ring's phase");
-static_assert(!(IKHIP_ANN_SPLIT_EPI && IKHIP_ANN_PREFETCH), "one layer-start scheme at a time");
-
-// chunk (m, j, fh) of a pass's accumulators: the activation in place (layer_store_h16's
-// pairs and order)
-template <int ACT, bool PIN = false, int MR, int NRP>
-__device__ __forceinline__ void epi_chunk(f32x4 (&c4)[MR][NRP][4], int m, int j, int fh,
-                                          float pre) {
-  f32x4 &a = c4[m][j][2 * fh];
-  f32x4 &b = c4[m][j][2 * fh + 1];
-  f32x2 t[4] = {f32x2{a.x, a.y}, f32x2{a.z, a.w}, f32x2{b.x, b.y}, f32x2{b.z, b.w}};
-  act_apply2x4<ACT>(t, pre);
-  a = f32x4{t[0].x, t[0].y, t[1].x, t[1].y};
-  b = f32x4{t[2].x, t[2].y, t[3].x, t[3].y};
-  // pinned here: left alone, the compiler sinks the chunk to its store after the barrier
-  if constexpr (PIN) asm volatile("" : "+v"(a), "+v"(b));
-}
-
-template <bool HOUT, int MR, int NRP>
-__device__ __forceinline__ void epi_put(float *H, const f32x4 (&c4)[MR][NRP][4], int nt0, int W,
-                                        int lane, int m, int j, int fh) {
-  const int col = (nt0 + W * j) * 32 + 16 * fh + 4 * (lane >> 4);
-#pragma unroll
-  for (int ph = 0; ph < 2; ++ph) {
-    const int row = m * 32 + 16 * ph + (lane & 15);
-    const f32x4 v = c4[m][j][2 * fh + ph];
-    if constexpr (HOUT) store_h4(H, row, col, v);
-    else *reinterpret_cast<f32x4 *>(H + row * kLd + col) = v;
-  }
-}
-
-// step_h16 with side work (a callable emitting VALU / transcendental instructions)
-// placed between the step's MFMAs: per pair of MFMAs one weight load and one LDS read
-// while they last, and up to two side instructions.
-template <int MR, int NR, int GI, typename Side>
-__device__ __forceinline__ void step_h16s(Split2 (&sa)[MR][2], const WStepH16<NR> &w,
-                                          WStepH16<NR> &fill, const WStream<NR> &ws,
-                                          const _Float16 *ab, int g, f32x4 (&acc)[MR][NR][4],
-                                          Side &&side) {
-  __builtin_amdgcn_sched_barrier(0);
-  load_wh16(fill, ws, g + kH16Ring - 1);
-  Split2 sn[MR][2];
-  load_ah16(sn, ab, GI + 1);
-  side();
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int j = 0; j < NR; ++j)
-#pragma unroll
-      for (int fh = 0; fh < 2; ++fh)
-#pragma unroll
-        for (int ph = 0; ph < 2; ++ph) {
-          f32x4 c = acc[m][j][2 * fh + ph];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].lo, c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][1], sa[m][ph].hi, c, 0, 0, 0);
-          acc[m][j][2 * fh + ph] =
-              __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].hi, c, 0, 0, 0);
-        }
-#pragma unroll
-  for (int i = 0; i < 6 * MR * NR; ++i) {
-    if (i < 4 * NR) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
-    if (i < 4 * MR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-    __builtin_amdgcn_sched_group_barrier(0x402, 2, 0);                  // VALU / TRANS
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int ph = 0; ph < 2; ++ph) sa[m][ph] = sn[m][ph];
-}
-
-// One K pass over NR column tiles nt0 + W j (layer_gemm_h16's loop; the first GS steps
-// unrolled, with side(step) between their MFMAs).  c4 comes back pre-scaled as there.
-template <int MR, int NR, int W, int GS, typename Side>
-__device__ __forceinline__ void h16_pass(const _Float16 *ap, const f16x8 *__restrict__ wx, int G32,
-                                         int xbytes, float xinv, int nt0, int lane,
-                                         const float *bias, f32x4 (&c4)[MR][NR][4], Side &&side) {
-  f32x4 bl[NR][2];
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int fh = 0; fh < 2; ++fh)
-      bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (nt0 + W * j) * 32 + 16 * fh +
-                                                   4 * (lane >> 4));
-  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
-  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, nt0, W, G32 * 4, lane);
-  WStepH16<NR> w[kH16Ring];
-#pragma unroll
-  for (int u = 0; u < kH16Ring - 1; ++u) load_wh16(w[u], ws, u);
-  const float scale = 1.0f / xinv;  // exact: xinv is 2^-k
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int fh = 0; fh < 2; ++fh) {
-      const f32x4 b = bl[j][fh] * scale;
-#pragma unroll
-      for (int m = 0; m < MR; ++m) c4[m][j][2 * fh] = c4[m][j][2 * fh + 1] = b;
-    }
-  Split2 sa[MR][2];
-  load_ah16(sa, ap, 0);
-  int g = 0;
-  if constexpr (GS > 0) {
-    static_for<GS>([&](auto s) {
-      constexpr int u = s.value % kH16Ring;
-      step_h16s<MR, NR, u>(sa, w[u], w[(u + kH16Ring - 1) % kH16Ring], ws,
-                           ap + 32 * (s.value - u), s.value, c4, [&] { side(s); });
-    });
-    g = GS;
-  }
-  for (; g + kH16Ring <= G32; g += kH16Ring) {
-    const _Float16 *ab = ap + 32 * g;
-    static_for<kH16Ring>([&](auto u) {
-      step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
-                                g + u.value, c4);
-    });
-  }
-  const _Float16 *ab = ap + 32 * g;
-  static_for<kH16Ring - 1>([&](auto u) {
-    if (g + u.value < G32)
-      step_h16<MR, NR, u.value>(sa, w[u.value], w[(u.value + kH16Ring - 1) % kH16Ring], ws, ab,
-                                g + u.value, c4);
-  });
-}
-
-// The layer (G32 >= kSplitSteps): P passes, then the barrier, the stores of the passes
-// already activated, and the last pass's epilogue.
-template <int MR, int P, int ACT, bool HOUT, int W>
-__device__ __forceinline__ void layer_h16_split(float *H, const f16x8 *__restrict__ wx, int G32,
-                                                int xbytes, float xinv, int wave, int lane,
-                                                const float *bias, unsigned long long *st) {
-  constexpr int NRP = 4 / P;
-  constexpr int C = MR * NRP * 2;  // chunks per pass
-  constexpr int every = kSplitSteps / C;
-  static_assert(kSplitSteps % C == 0, "chunks spread evenly over the unrolled steps");
-  const _Float16 *ap =
-      hplane(H, lane & 15) + ((8 * (lane >> 4)) ^ hswz(lane & 15));
-  f32x4 c4[P][MR][NRP][4];
-  static_for<P>([&](auto p) {
-    constexpr int pv = p.value;
-    if constexpr (pv == 0) {
-      h16_pass<MR, NRP, W, 0>(ap, wx, G32, xbytes, xinv, wave, lane, bias, c4[0], [](auto) {});
-    } else {
-      h16_pass<MR, NRP, W, kSplitSteps>(
-          ap, wx, G32, xbytes, xinv, wave + W * NRP * pv, lane, bias, c4[pv], [&](auto s) {
-            if constexpr (s.value % every == 0) {
-              constexpr int c = s.value / every;
-              epi_chunk<ACT, true>(c4[pv - 1], c / (NRP * 2), (c >> 1) % NRP, c & 1, xinv);
-            }
-          });
-    }
-  });
-  stamp(st);
-  __syncthreads();  // every wave has finished reading the layer input
-  static_for<P - 1>([&](auto p) {
-#pragma unroll
-    for (int j = 0; j < NRP; ++j)
-#pragma unroll
-      for (int fh = 0; fh < 2; ++fh)
-#pragma unroll
-        for (int m = 0; m < MR; ++m)
-          epi_put<HOUT>(H, c4[p.value], wave + W * NRP * p.value, W, lane, m, j, fh);
-  });
-#pragma unroll
-  for (int j = 0; j < NRP; ++j)
-#pragma unroll
-    for (int fh = 0; fh < 2; ++fh)
-#pragma unroll
-      for (int m = 0; m < MR; ++m) {
-        epi_chunk<ACT>(c4[P - 1], m, j, fh, xinv);
-        epi_put<HOUT>(H, c4[P - 1], wave + W * NRP * (P - 1), W, lane, m, j, fh);
-      }
-}
-
-template <int MR, int W>
-__device__ __forceinline__ void run_layer_h16_split(float *H, const void *wx, int G32, int NT,
-                                                    float xinv, int wave, int lane,
-                                                    const float *bias, int act, bool hout,
-                                                    unsigned long long *st) {
-  constexpr int P = IKHIP_ANN_SPLIT_EPI ? IKHIP_ANN_SPLIT_EPI : 2;
-  const f16x8 *w = static_cast<const f16x8 *>(wx);
-  const int xb = NT * G32 * 4 * 1024;
-  if (act == IK_ACT_TANH) {
-    if (hout) layer_h16_split<MR, P, IK_ACT_TANH, true, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
-    else layer_h16_split<MR, P, IK_ACT_TANH, false, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
-  } else {
-    if (hout) layer_h16_split<MR, P, IK_ACT_SIGMOID, true, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
-    else layer_h16_split<MR, P, IK_ACT_SIGMOID, false, W>(H, w, G32, xb, xinv, wave, lane, bias, st);
-  }
 }
 
 // bf16x6 on v_mfma_f32_16x16x32_bf16 (IKHIP_ANN_X16): the same six products in
@@ -1337,13 +1053,13 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
 // a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
 // layer is one) stores the activations as split planes.
-template <int ACT, bool HOUT, int W, int X, bool PF, int MR, int NR>
+template <int ACT, bool HOUT, int W, int X, int MR, int NR>
 __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[NR], int wave,
                                           int lane, f32x16 (&acc)[MR][NR],
-                                          unsigned long long *st, float pre, PreH16 *pf) {
+                                          unsigned long long *st, float pre) {
   if (tr) {
     if constexpr ((X == 2 && kH16) || (X == 1 && kX16))
-      layer_store_h16<MR, NR, ACT, HOUT, W, PF>(H, wave, lane, acc, st, pre, pf);
+      layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st, pre);
     else layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
   } else {
     layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
@@ -1352,26 +1068,24 @@ __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[N
 
 // pre: the fp16x3 16x16x32 GEMM's accumulators still carry the weight pre-scale
 // (layer_gemm_h16); 1 for every other layer.
-template <bool HOUT, int W, int X, bool PF = false, int MR, int NR>
+template <bool HOUT, int W, int X, int MR, int NR>
 __device__ __forceinline__ void store_act(int act, bool tr, float *H, const float (&bv)[NR],
                                           int wave, int lane, f32x16 (&acc)[MR][NR],
-                                          unsigned long long *st, float pre = 1.0f,
-                                          PreH16 *pf = nullptr) {
+                                          unsigned long long *st, float pre = 1.0f) {
   switch (act) {
-    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
-    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
-    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
-    default: store_any<IK_ACT_LINEAR, HOUT, W, X, PF>(tr, H, bv, wave, lane, acc, st, pre, pf); break;
+    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    default: store_any<IK_ACT_LINEAR, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
   }
 }
 
-template <int MR, int NR, int X = 0, bool HX = false, int W = kWaves, bool PF = false>
+template <int MR, int NR, int X = 0, bool HX = false, int W = kWaves>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           unsigned long long *st_first,
                                           const void *wx = nullptr, int G16 = 0,
-                                          float xinv = 1.0f, bool hout = false,
-                                          PreH16 *pf = nullptr) {
+                                          float xinv = 1.0f, bool hout = false) {
   f32x16 acc[MR][NR];
   const int NT = wbytes / (G * 1024);  // column tiles of the layer
   float bv[NR];
@@ -1386,8 +1100,8 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
                                 wave, lane, bias, acc);
     }
     else if constexpr (kH16)  // G16: 32-deep K steps here
-      layer_gemm_h16<MR, NR, W, PF>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
-                                xinv, wave, lane, bias, acc, st_first, pf);
+      layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
+                                xinv, wave, lane, bias, acc, st_first);
     else
       layer_gemm_h<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024,
                               xinv, wave, lane, bias, acc);
@@ -1397,8 +1111,8 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
     layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, W, lane, nullptr, acc, st_first);
   }
   const float pre = (X == 2 && kH16 && tr) ? xinv : 1.0f;
-  if (HX && hout) store_act<true, W, X, PF>(act, tr, H, bv, wave, lane, acc, st, pre, pf);
-  else store_act<false, W, X, PF>(act, tr, H, bv, wave, lane, acc, st, pre, pf);
+  if (HX && hout) store_act<true, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
+  else store_act<false, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
 }
 
 // HOUT: the next layer runs fp16x3, so the result goes out as split planes
@@ -1511,12 +1225,9 @@ ann_fused_kernel(AnnArgs a) {
   // + kHPad: the fp32 GEMM's operand ring reads up to 3 K groups past a row's end
   __shared__ __attribute__((aligned(16))) float H[BM * kLd + kHPad];
   const int tid = threadIdx.x;
-#ifndef IKHIP_ANN_UNIFORM_WAVE
-#define IKHIP_ANN_UNIFORM_WAVE 1
-#endif
   // wave index in an SGPR: the per-wave column-tile count (cnt) and the paths it
-  // selects are then uniform branches, not exec-masked regions
-  const int wave = IKHIP_ANN_UNIFORM_WAVE ? __builtin_amdgcn_readfirstlane(tid >> 6) : tid >> 6;
+  // selects are uniform branches, not exec-masked regions
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63;
   const int64_t ntiles = (a.n + BM - 1) / BM;
   double blk_max = 0.0, blk_sum = 0.0;  // FK round-trip error of this lane's points
@@ -1565,16 +1276,13 @@ ann_fused_kernel(AnnArgs a) {
     __syncthreads();
     stamp(stp ? stp + 1 : nullptr);
     // ---- Dense layers
-    PreH16 pf;  // IKHIP_ANN_PREFETCH: the next layer's first weight step
     for (int l = 0; l < a.m.n_layers; ++l) {
-#ifndef IKHIP_ANN_LAUNDER
-#define IKHIP_ANN_LAUNDER 1
-#endif
       // an opaque (always 0) uniform offset on the LDS tile per layer: the layer
-      // functions' per-lane LDS addresses are then recomputed per layer instead of
-      // being hoisted out of the tile loop and held in registers across it
+      // functions' per-lane LDS addresses are recomputed per layer instead of being
+      // hoisted out of the tile loop and held in registers across it (fp16x3 kernel:
+      // 503 -> 396 registers; bf16x6 -1.2 %, the others even)
       int hz = 0;
-      if (IKHIP_ANN_LAUNDER) asm volatile("" : "+s"(hz));
+      asm volatile("" : "+s"(hz));
       float *const HL = H + hz;
       const int G = a.m.kp[l] >> 3;
       const int NT = a.m.np[l] >> 5;
@@ -1589,36 +1297,15 @@ ann_fused_kernel(AnnArgs a) {
                         (a.m.np[l + 1] >> 5) > 1;
       if (NT == 1) {
         run_layer_splitk<MR, X == 2, W>(HL, wp, bias, act, G, wave, lane, tid, sl, hout);
-        pf.drop();
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
         // K steps of the split GEMM: 16 deep (bf16x6, 32x32x16 fp16x3), 32 (16x16x32)
         const int G16 =
             ((X == 2 && kH16) || (X == 1 && kX16)) ? (a.m.kp[l] + 31) >> 5 : (a.m.kp[l] + 15) >> 4;
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
-        bool pref_ok = false;
-        if constexpr (X == 2 && kH16 && IKHIP_ANN_PREFETCH && W * 4 <= 16) {
-          // the next layer takes the same path with 4 column tiles on every wave
-          const int ln = l + 1;
-          pref_ok = cnt == 4 && ln < a.m.n_layers && a.m.wx[ln] != nullptr &&
-                    (a.m.np[ln] >> 5) == 4 * W;
-          pf.want = pref_ok;
-          if (pref_ok) {
-            pf.nwx = a.m.wx[ln];
-            pf.nG32 = (a.m.kp[ln] + 31) >> 5;
-            pf.nxbytes = (a.m.np[ln] >> 5) * pf.nG32 * 4 * 1024;
-            pf.nbias = a.m.bias[ln];
-          }
-        }
         switch (cnt) {
           case 4:
-            if constexpr (X == 2 && kH16 && IKHIP_ANN_SPLIT_EPI && W * 4 <= 16) {
-              if (G16 >= kSplitSteps && (act == IK_ACT_TANH || act == IK_ACT_SIGMOID)) {
-                run_layer_h16_split<MR, W>(HL, wx, G16, NT, xinv, wave, lane, bias, act, hout, sl);
-                break;
-              }
-            }
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W, X == 2 && kH16 && IKHIP_ANN_PREFETCH>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout, &pf);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
             break;
           case 3:
             if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
@@ -1627,9 +1314,7 @@ ann_fused_kernel(AnnArgs a) {
           case 1: run_layer<MR, 1, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
           default: __syncthreads(); break;
         }
-        if (cnt != 4) pf.drop();
       } else {
-        pf.drop();
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
