@@ -19,7 +19,13 @@ def main():
         for call in range(2):
             ang, it, err, _ = ctx.fabrik_solve_fk(pts, tol, mi)
             h = hashlib.sha256(ang.tobytes() + it.tobytes() + err.tobytes()).hexdigest()[:16]
-            print(f"tol {tol:g} call {call} iters {int(it.sum())} {h}")
+            if os.environ.get("FAB_BITCMP_SPLIT"):  # angles + iterations apart from the FK errors
+                hai = hashlib.sha256(ang.tobytes() + it.tobytes()).hexdigest()[:16]
+                ok = err == err
+                print(f"tol {tol:g} call {call} iters {int(it.sum())} max_err {err[ok].max():.17g} "
+                      f"sum_err {err[ok].sum():.17g} angles+iters {hai}")
+            else:
+                print(f"tol {tol:g} call {call} iters {int(it.sum())} {h}")
 
 
 if __name__ == "__main__":
