@@ -94,7 +94,7 @@ def maybe_launch(argv=None):
     return subprocess.call(launch_command(argv, gpus, port), env=env)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -128,7 +128,12 @@ def parse():
     ap.add_argument("--total-points", type=int, default=0,
                     help="global batch sharded over the ranks (strong scaling; configs[3] / "
                          "configs[4] are 10000000); 0 = --points per GPU (weak scaling)")
-    return ap.parse_args()
+    ap.add_argument("--strong-legs", type=int, default=1,
+                    help="N>1 with the weak headline: also time configs[3] (ANN fp32 + FK "
+                         "round trip) and configs[4] (FABRIK tol 1e-5 / 200) as BASELINE.json "
+                         "states them, the 10M-point seed-1 batch sharded over the N ranks, "
+                         "under 'secondary' (VERDICT r04 #1)")
+    return ap.parse_args(argv)
 
 
 def dist_setup(args):
@@ -435,6 +440,10 @@ def run_ann(job, args, mode="fp32"):
 
     res = timed(ctx, step, args, world)
     st = ctx.stats_fetch()
+    mx, sm, _, _ = _stats_over_ranks(job, st, res)
+    # the p99 from the last sharded step's gathered histograms, BEFORE the gather
+    # check's plain re-solves (a plain call ends the sharded call's state: ADVICE r04)
+    res["p99_fk_err"] = _p99(job, derr, world)
     if job.sc is not None:
         res["gather_chunks"] = job.sc.info()[2]
         res["gather_ms"] = st.gather_ms
@@ -445,10 +454,8 @@ def run_ann(job, args, mode="fp32"):
                                                                device="cuda"))
             return {"ang": a}
         res["gather_check"] = gather_check(job, {"ang": dang}, resolve)
-    mx, sm, _, _ = _stats_over_ranks(job, st, res)
     res["max_fk_err"] = mx
     res["mean_fk_err"] = sm / job.total
-    res["p99_fk_err"] = _p99(job, derr, world)
     res["fk_err_note"] = ("random Glorot weights (the reference .h5 is not shipped): the FK "
                           "round trip is computed in the same launch; not model accuracy")
     res["outputs"] = {"ang": dang}
@@ -506,22 +513,28 @@ def run_fabrik(job, args, tol=None, max_iter=None):
 
     # the --verbose FK round trip (cli.py:54-72) in the same launch as the angles
     if job.sc is not None:
-        def solve(p, a, i, e):  # solve the shard + the library's one RCCL all-gather
+        def solve(p, a, i, e):  # solve the shard + the library's RCCL all-gathers
             job.sc.fabrik_device(p, a, i, e, tol, max_iter, flags=flags)
         batch = job.dpts
+        # the timed step gathers what the reference returns, the angles
+        # (inverse.py:139: 32 B a row); the iteration counts travel only in the
+        # untimed call after the timed steps
+        step_it = None
     else:
         def solve(p, a, i, e):
             ctx.fabrik_solve_device(p, a, i, None, tol, max_iter, flags=flags, fk_err=e)
         batch = job.local_pts
+        step_it = dit
 
     def step():
-        solve(batch, dang, dit, derr)
+        solve(batch, dang, step_it, derr)
 
     # the warm-up steps teach the work-order table on ANOTHER batch of the same
     # distribution (seed 2), so the timed steps do not start from a table
     # learned on their own points
     wpts = torch.from_numpy(warm_batch(batch.shape[0])).cuda()
-    wang, wit, werr = torch.empty_like(dang), torch.empty_like(dit), torch.empty_like(derr)
+    wang, werr = torch.empty_like(dang), torch.empty_like(derr)
+    wit = None if step_it is None else torch.empty_like(dit)
 
     def warm():
         solve(wpts, wang, wit, werr)
@@ -539,11 +552,20 @@ def run_fabrik(job, args, tol=None, max_iter=None):
     res = timed(ctx, step, args, world, warm=warm, after_warm=after_warm)
     res["order_table"] = table
     del wpts, wang, wit, werr
-    st = ctx.stats_fetch()
     if job.sc is not None:
         res["gather_chunks"] = job.sc.info()[2]
-        res["gather_ms"] = st.gather_ms
-
+        res["gather_ms"] = ctx.stats_fetch().gather_ms  # the last timed step's gathers
+        res["gathered_bytes_per_row"] = 32
+        # untimed: the same sharded call with the iteration counts gathered too
+        # (the rows are the timed steps' own: the solve is deterministic)
+        solve(batch, dang, dit, derr)
+        ctx.sync()
+    st = ctx.stats_fetch()
+    mx, sm, sum_iters, n_capped = _stats_over_ranks(job, st, res)
+    # the p99 from the last sharded call's gathered histograms, BEFORE the gather
+    # check's plain re-solves (a plain call ends the sharded call's state: ADVICE r04)
+    res["p99_fk_err"] = _p99(job, derr, world)
+    if job.sc is not None:
         def resolve(b, e):
             a = torch.empty((e - b, 4), dtype=torch.float64, device="cuda")
             i = torch.empty(e - b, dtype=torch.int32, device="cuda")
@@ -551,7 +573,6 @@ def run_fabrik(job, args, tol=None, max_iter=None):
                                     fk_err=torch.empty(e - b, dtype=torch.float64, device="cuda"))
             return {"ang": a, "iters": i}
         res["gather_check"] = gather_check(job, {"ang": dang, "iters": dit}, resolve)
-    mx, sm, sum_iters, n_capped = _stats_over_ranks(job, st, res)
     if args.cold:
         res["cold"] = cold_steps(ctx, step)
     n = job.n_local
@@ -559,7 +580,6 @@ def run_fabrik(job, args, tol=None, max_iter=None):
     res["n_capped"] = int(n_capped)
     res["max_fk_err"] = mx
     res["mean_fk_err"] = sm / job.total
-    res["p99_fk_err"] = _p99(job, derr, world)
     res["outputs"] = {"ang": dang, "iters": dit}
     if args.end_to_end:
         res["end_to_end"] = end_to_end(
@@ -901,6 +921,56 @@ def _config_ref(method, total, world, tol, max_iter):
     return None
 
 
+STRONG_POINTS = 10_000_000  # configs[3] / configs[4]: 10M points over the N GPUs
+
+
+def strong_legs():
+    """The N > 1 strong-scaling legs: secondary key -> runner.
+    Their keys end in '_strong10M'; the method and settings are in the name."""
+    return {"ann_strong10M": lambda j, a: run_ann(j, a, mode="fp32"),
+            "fabrik_tol1e-5_strong10M": lambda j, a: run_fabrik(j, a, tol=1e-5, max_iter=200)}
+
+
+def leg_settings(key, args):
+    """(method, tol, max_iter) a secondary key measures."""
+    method = "fabrik" if key.startswith("fabrik") else ("ann" if key.startswith("ann") else key)
+    if key.startswith("fabrik_tol1e-5"):
+        return method, 1e-5, 200
+    return method, args.tol, args.max_iter
+
+
+def secondary_entry(key, r2, total, world, args):
+    """One method's entry under the line's 'secondary', labelled with the
+    BASELINE.json config it measures (_config_ref), if any."""
+    e = {"value": r2.get("total", total) / (r2["ms_per_step"] / 1e3),
+         "unit": r2.get("unit", "IK solutions/s"),
+         "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
+         "roofline": r2["roofline"], "workload": r2["workload"],
+         "kernels_ms": r2["kernels"], "total_points": r2.get("total", total),
+         **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err", "mean_iters",
+                               "n_capped", "end_to_end", "gather_chunks", "gather_ms", "cold",
+                               "gather_check", "order_table", "gathered_bytes_per_row")
+            if k in r2}}
+    method, tol, max_iter = leg_settings(key, args)
+    if method == "ann" and key not in ("ann", "ann_strong10M"):
+        return e  # the split modes: no BASELINE config names them
+    cref = _config_ref(method, total, world, tol, max_iter)
+    if cref:
+        e["baseline_config"] = cref
+    return e
+
+
+def strong_job(ctx, sc, world, rank, total):
+    """The configs[3] / configs[4] batch (random_dist, seed 1) on every rank, this
+    rank's shard of it, on the same context and communicator as the headline."""
+    import torch
+    from inversekinematicsann_amd import dist as D
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    pts = random_dist(total, seed=1)
+    lo, hi = D.shard_bounds(total, world, rank)
+    return Job(ctx, sc, pts, torch.from_numpy(pts).cuda(), lo, hi, world)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -955,22 +1025,20 @@ def main():
         for other in others:
             r2 = runners[other](job, args)
             checks[other] = r2.get("gather_check")
-            secondary[other] = {"value": r2.get("total", total) / (r2["ms_per_step"] / 1e3),
-                                "unit": r2.get("unit", "IK solutions/s"),
-                                "ms_per_step": r2["ms_per_step"], "dtype": r2["dtype"],
-                                "roofline": r2["roofline"], "workload": r2["workload"],
-                                "kernels_ms": r2["kernels"],
-                                **{k: r2[k] for k in ("max_fk_err", "mean_fk_err", "p99_fk_err",
-                                                      "mean_iters", "n_capped", "end_to_end",
-                                                      "gather_chunks", "gather_ms", "cold",
-                                                      "gather_check", "order_table")
-                                   if k in r2}}
-            cref = _config_ref("fabrik" if other.startswith("fabrik") else other, total, world,
-                               1e-5 if other == "fabrik_tol1e-5" else args.tol,
-                               200 if other == "fabrik_tol1e-5" else args.max_iter)
-            if cref:
-                secondary[other]["baseline_config"] = cref
+            secondary[other] = secondary_entry(other, r2, total, world, args)
             outputs[other] = r2["outputs"]
+    if world > 1 and not strong and args.strong_legs and args.method != "fk":
+        # configs[3] / configs[4] as BASELINE.json states them: the 10M-point seed-1
+        # batch sharded over the N ranks (strong scaling), beside the weak headline
+        sjob = strong_job(ctx, sc, world, rank, STRONG_POINTS)
+        sargs = argparse.Namespace(**{**vars(args), "end_to_end": 0, "cold": 0})
+        for key, fn in strong_legs().items():
+            r2 = fn(sjob, sargs)
+            checks[key] = r2.get("gather_check")
+            secondary[key] = secondary_entry(key, r2, STRONG_POINTS, world, sargs)
+            secondary[key]["scaling"] = "strong"
+            del r2
+        del sjob
     gcheck, exit_code = gather_verdict(checks)
     value = res.get("total", total) / (res["ms_per_step"] / 1e3)
     line = {
@@ -997,6 +1065,8 @@ def main():
                    "n_ranks_rccl": sc.info()[0] if sc is not None else None,
                    "gather_chunks": res.get("gather_chunks"),
                    "gather_check": gcheck,
+                   "strong_legs": ({k: secondary[k].get("baseline_config") for k in strong_legs()
+                                    if k in secondary} or None),
                    "tol": args.tol if args.method == "fabrik" else None,
                    "max_iter": args.max_iter if args.method == "fabrik" else None},
         "roofline": res["roofline"],

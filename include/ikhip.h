@@ -139,10 +139,11 @@ int ik_fabrik_order_get(ik_ctx *ctx, uint32_t *key, int n);
 int ik_fabrik_order_set(ik_ctx *ctx, const uint32_t *key, int n);
 
 /* Fabrik.calculate, kinematics/fabrik.py:44-67, batched over n goals for a chain
- * of nj (1..2^20) joints: init is n x nj x 3 (or nj x 3 shared by all goals when
+ * of nj (1..4096) joints: init is n x nj x 3 (or nj x 3 shared by all goals when
  * init_shared != 0), goals n x 3 -> joints n x nj x 3, iters n (nullable).
  * 2..8 joints run with the chain in registers; other lengths keep it in the
- * joints output row (same arithmetic, same bits). */
+ * joints output row (same arithmetic, same bits) at about nj * max_iter * 2
+ * dependent steps of ~0.4 us per goal (4096 joints x 100 iterations: ~0.3 s). */
 int ik_fabrik_calc(ik_ctx *ctx, int nj, const double *dists, const double *init,
                    int init_shared, const double *goals, int64_t n, double tol,
                    int32_t max_iter, double *joints, int32_t *iters, int flags,
@@ -299,8 +300,9 @@ int ik_comm_destroy(ik_ctx *ctx);
  * count the last sharded call was planned with (ik_shard_plan_of's chunks; 0
  * before one), so a caller can find its own rows with ik_shard_part. */
 int ik_comm_info(ik_ctx *ctx, int *nranks, int *rank, int *last_chunks);
-/* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic (1: one
- * in-place all-gather after the solve).  Every rank must use the same value:
+/* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic: ANN 1
+ * (one in-place all-gather after the solve), FABRIK 2 when nranks > 1 (chunk 0's
+ * gather under chunk 1's solve).  Every rank must use the same value:
  * each call's tail carries its plan (n, chunks, method) and a rank whose plan
  * differs from rank 0's fails the call with IK_E_RCCL.  Environment default:
  * IKHIP_GATHER_CHUNKS (checked equal on every rank by ik_comm_init). */

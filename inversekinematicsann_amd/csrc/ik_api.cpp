@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -433,7 +434,13 @@ int ik_ctx_sync(ik_ctx *c) {
   if (c->last_piped) return IK_OK;  // a chunked host pipeline returns complete
   if (!c->call_done_set) return IK_OK;
   // with a communicator the wait is bounded (its deadline and async errors)
-  return comm_wait(c, c->call_done, "the last call");
+  rc = comm_wait(c, c->call_done, "the last call");
+  if (rc) return rc;
+  // an IK_F_ASYNC sharded call is validated here as ik_stats_fetch would: every
+  // rank planned the same (n, chunks, method), else the gathered rows belong to
+  // another plan
+  if (c->last_sharded) return sharded_stats(c, nullptr);
+  return IK_OK;
 }
 
 int ik_stats_fetch(ik_ctx *c, ik_stats *stats) {
@@ -617,8 +624,15 @@ int ik_fabrik_reset_order(ik_ctx *c) {
 int ik_fabrik_order_get(ik_ctx *c, uint32_t *key, int n) {
   if (!c || !key || n < kOrdCells) return -fail(IK_E_BADARG, "ik_fabrik_order_get: bad args");
   if (set_dev(c)) return -IK_E_HIP;
-  if (hipStreamSynchronize(c->last_stream ? c->last_stream : c->stream) != hipSuccess ||
-      hipMemcpy(key, c->fab_ord->key, sizeof(c->fab_ord->key), hipMemcpyDeviceToHost) != hipSuccess)
+  // the last call's end, waited for with the communicator's deadline when one is
+  // bound (a dead peer ends the wait with IK_E_RCCL instead of hanging it)
+  if (c->call_done_set) {
+    const int rc = comm_wait(c, c->call_done, "the last call");
+    if (rc) return -rc;
+  } else if (hipStreamSynchronize(c->stream) != hipSuccess) {
+    return -fail(IK_E_HIP, "ik_fabrik_order_get: stream synchronize failed");
+  }
+  if (hipMemcpy(key, c->fab_ord->key, sizeof(c->fab_ord->key), hipMemcpyDeviceToHost) != hipSuccess)
     return -fail(IK_E_HIP, "ik_fabrik_order_get: copy failed");
   return kOrdCells;
 }
@@ -744,24 +758,44 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
       total = (total + 255) & ~(size_t)255;
     }
   }
-  std::vector<char> host(total, 0);
-  for (int l = 0; l < n_layers; ++l) {
-    ann_pack_layer(W[l], dims[l], dims[l + 1], reinterpret_cast<float *>(&host[woff[l]]));
-    std::memcpy(&host[boff[l]], b[l], (size_t)dims[l + 1] * 4);
-    if (splittable(l))
-      ann_pack_layer_x(W[l], dims[l], dims[l + 1], &host[xoff[l]]);
-    if (halvable(l)) {
-      hexp[l] = ann_h_scale_exp(W[l], dims[l], dims[l + 1]);
-      ann_pack_layer_h(W[l], dims[l], dims[l + 1], hexp[l], &host[hoff[l]]);
-    }
-  }
+  // (the widths and depth are capped above, so `total` stays far below 2^64: at
+  // most 4096 layers of a 16384 x 16384 product, ~4.4 TB -- but that may not fit
+  // the device, and the host staging must not be one buffer of that size)
   IK_HIP(hipStreamSynchronize(c->stream));
   if (c->ann_buf) IK_HIP(hipFree(c->ann_buf));
   c->ann_buf = nullptr;
   c->ann_loaded = false;
+  size_t dev_free = 0, dev_total = 0;
+  IK_HIP(hipMemGetInfo(&dev_free, &dev_total));
+  if (total > dev_free)
+    return fail(IK_E_HIP, "ik_ann_load: the packed model needs " + std::to_string(total) +
+                              " bytes of device memory, " + std::to_string(dev_free) +
+                              " are free");
   IK_HIP(hipMalloc(&c->ann_buf, total));
-  IK_HIP(hipMemcpy(c->ann_buf, host.data(), total, hipMemcpyHostToDevice));
   char *base = static_cast<char *>(c->ann_buf);
+  // pack and upload one layer's section at a time: the host holds
+  // at most the largest layer's packed bytes, and an allocation failure is an
+  // error code, not an exception leaving the C ABI
+  try {
+    std::vector<char> host;
+    for (int l = 0; l < n_layers; ++l) {
+      const size_t end = l + 1 < n_layers ? woff[l + 1] : total;
+      host.assign(end - woff[l], 0);
+      char *h = host.data();  // the section starts at woff[l] in the model buffer
+      ann_pack_layer(W[l], dims[l], dims[l + 1], reinterpret_cast<float *>(h));
+      std::memcpy(h + (boff[l] - woff[l]), b[l], (size_t)dims[l + 1] * 4);
+      if (splittable(l)) ann_pack_layer_x(W[l], dims[l], dims[l + 1], h + (xoff[l] - woff[l]));
+      if (halvable(l)) {
+        hexp[l] = ann_h_scale_exp(W[l], dims[l], dims[l + 1]);
+        ann_pack_layer_h(W[l], dims[l], dims[l + 1], hexp[l], h + (hoff[l] - woff[l]));
+      }
+      IK_HIP(hipMemcpy(base + woff[l], host.data(), host.size(), hipMemcpyHostToDevice));
+    }
+  } catch (const std::bad_alloc &) {
+    (void)hipFree(c->ann_buf);
+    c->ann_buf = nullptr;
+    return fail(IK_E_HIP, "ik_ann_load: out of host memory staging the packed weights");
+  }
   c->ann_big = big;
   c->ann_bigm.layers.clear();
   if (big) {

@@ -508,8 +508,13 @@ void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, dou
 // FK of a chain of nj (2..kFkMaxJoints) joints; dh: device 4 x nj, mats nullable
 // n x nj x 16 (2..8 unrolled, longer chains a run-time joint loop).
 constexpr int kFkMaxJoints = 1024;
-// Fabrik.calculate's chain length bound (ik_fabrik_calc)
-constexpr int kCalcMaxJoints = 1 << 20;
+// Fabrik.calculate's chain length bound (ik_fabrik_calc).  Chains past 8 joints
+// run one goal per lane with the chain in its output row, so a goal costs about
+// nj * max_iter * 2 dependent point_between steps (~0.4 us each, an L2 round
+// trip): 4096 joints at 100 iterations is ~0.3 s for a launch of any width
+// (tests/test_gpu_parity.py::test_fabrik_calc_longest_chain), well inside the
+// GPU's hang detection; longer chains are refused.
+constexpr int kCalcMaxJoints = 4096;
 void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double *xyz,
                  double *mats, DevStats *S, hipStream_t st);
 // FABRIK work order (ik_fabrik.hip "Work order"): per context, the largest

@@ -388,14 +388,17 @@ int auto_chunks(ik_ctx *c, int method, int64_t n) {
   const IkComm &m = c->comm;
   int C = m.chunks_req;
   if (C <= 0) C = env_chunks();
-  // automatic: one chunk.  Chunked gathers under the next chunk's solve are
-  // opt-in (ik_comm_set_chunks / IKHIP_GATHER_CHUNKS, the same on every rank:
-  // ik_comm_init checks the environment's, every call's tail its plan) until a
-  // run of two or more real ranks has checked them bit for bit against a plain
-  // solve; the one-chunk pattern is one in-place all-gather.
-  (void)method;
+  // automatic (DESIGN.md §5's gather model): ANN one chunk -- its gather is
+  // ~0.5 % of the solve, a second launch tail would cost more than the overlap
+  // saves; FABRIK two chunks at g > 1 -- its 32-byte rows gather in about the
+  // solve's time at 8 ranks, and chunk 0's gather then runs under chunk 1's
+  // solve (predicted 0.62 against 0.76 ms a step, configs[4] at 8 ranks).  The
+  // plan depends only on (n, g, method) and the explicit setting, so every rank
+  // makes the same one (ik_comm_init checks the environment's, every call's
+  // tail its plan); bench.py's gather check compares the gathered rows with a
+  // plain re-solve bit for bit on every N > 1 run.
   (void)n;
-  if (C <= 0) C = 1;
+  if (C <= 0) C = (method == IK_METHOD_FABRIK && m.nranks > 1) ? 2 : 1;
   return C > IK_MAX_GATHER_CHUNKS ? IK_MAX_GATHER_CHUNKS : C;
 }
 

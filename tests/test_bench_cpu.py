@@ -165,3 +165,37 @@ def test_roofline_fracs_headline_the_lower():
     fr = bench.roofline_fracs(100.0, 2000.0, 1000.0, {})
     assert fr["headline"] == "events" and fr["frac_rocprof"] is None
     assert bench.roofline_fracs(100.0, None, 1000.0, {})["headline"] is None
+
+
+def test_strong_legs_are_configs_3_and_4_at_world_8():
+    """at N > 1 the bench adds configs[3] (ANN fp32 + FK round trip)
+    and configs[4] (FABRIK tol 1e-5 / 200) on the 10M-point batch sharded over the
+    ranks, labelled by _config_ref; the weak headline stays configs[1] / [2] and
+    one GPU never labels a line configs[3] / [4]."""
+    import bench
+    args = bench.parse(["--gpus", "8"])
+    assert args.strong_legs == 1 and args.total_points == 0
+    legs = bench.strong_legs()
+    assert set(legs) == {"ann_strong10M", "fabrik_tol1e-5_strong10M"}
+    assert bench.STRONG_POINTS == 10_000_000
+    r2 = {"ms_per_step": 50.0, "dtype": "fp32", "roofline": {}, "workload": "w", "kernels": {}}
+    e = bench.secondary_entry("ann_strong10M", r2, bench.STRONG_POINTS, 8, args)
+    assert e["baseline_config"] == "configs[3]" and e["total_points"] == 10_000_000
+    assert abs(e["value"] - 10_000_000 / 0.05) < 1e-3
+    e = bench.secondary_entry("fabrik_tol1e-5_strong10M", dict(r2, dtype="f64"),
+                              bench.STRONG_POINTS, 8, args)
+    assert e["baseline_config"] == "configs[4]"
+    assert bench.leg_settings("fabrik_tol1e-5_strong10M", args) == ("fabrik", 1e-5, 200)
+    # the weak legs at world 8 (1M per GPU) and the split modes
+    assert bench.secondary_entry("fabrik", r2, 8_000_000, 8, args)["baseline_config"] == \
+        "configs[2]"
+    assert "baseline_config" not in bench.secondary_entry("fabrik_tol1e-5", r2, 8_000_000, 8,
+                                                          args)
+    assert "baseline_config" not in bench.secondary_entry("ann_fp16x3", r2, 8_000_000, 8, args)
+    assert bench._config_ref("ann", 8_000_000, 8, 1e-3, 100) == "configs[1]"
+    # one GPU: never configs[3] / [4], whatever the batch
+    assert bench._config_ref("ann", 10_000_000, 1, 1e-3, 100) is None
+    assert bench._config_ref("fabrik", 10_000_000, 1, 1e-5, 200) is None
+    for w in (2, 4):
+        assert bench._config_ref("ann", 10_000_000, w, 1e-3, 100) == "configs[3]"
+        assert bench._config_ref("fabrik", 10_000_000, w, 1e-5, 200) == "configs[4]"

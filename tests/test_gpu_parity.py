@@ -193,6 +193,32 @@ def test_fabrik_calc_any_length(ctx1, nj):
     assert np.array_equal(it2, rit) and np.abs(out2 - rout).max() <= 1e-9
 
 
+def test_fabrik_calc_longest_chain(ctx1):
+    """the documented upper length (4096 joints, ikhip.h) runs in
+    well under a second for a handful of goals at 100 iterations and matches the
+    oracle (bit-exact iteration counts, joints within 1e-9); 4097 joints are refused
+    with IK_E_BADARG instead of becoming a multi-second kernel."""
+    import time
+    from inversekinematicsann_amd import _native
+    nj = 4096
+    links = np.full(nj, 0.01)
+    init = np.zeros((nj, 3))
+    init[:, 2] = np.arange(nj) * 0.01
+    goals = np.array([[5.0, 3.0, 20.0], [-4.0, 2.0, 30.0], [0.5, 0.5, 40.0], [30.0, 0.0, 1.0]])
+    t0 = time.perf_counter()
+    out, it, st = ctx1.fabrik_calc(links, init, goals, 1e-3, 100)
+    secs = time.perf_counter() - t0
+    rout, rit, rst = O.fabrik_calc(np.broadcast_to(init, (len(goals), nj, 3)), goals, links,
+                                   1e-3, 100)
+    assert st.first_err == -1 and (rst == O.OK).all()
+    assert np.array_equal(it, rit) and it.max() > 1
+    assert np.abs(out - rout).max() <= 1e-9
+    assert secs < 5.0, secs
+    with pytest.raises(_native.NativeError) as ei:
+        ctx1.fabrik_calc(np.full(nj + 1, 0.01), np.zeros((nj + 1, 3)), goals[:1], 1e-3, 10)
+    assert ei.value.code == _native.IK_E_BADARG
+
+
 def test_fabrik_calc_any_length_zero_division(ctx1):
     """A zero-length segment raises ZeroDivisionError in the reference
     (point.py:40-43): a goal on the chain's second-to-last joint makes the first
