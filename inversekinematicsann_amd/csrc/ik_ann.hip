@@ -196,13 +196,9 @@ __device__ __forceinline__ T wload(const WStream<NR> &w, int j, int blk) {
   return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b128(w.rs, w.vo[j], blk * 1024, 0));
 }
 
-// TR: weights as the A operand and activations as B, so the accumulator holds
-// C^T -- a lane owns one point (column lane & 31) and 16 of its outputs
-// (rows (q & 3) + 8 (q >> 2) + 4 (lane >> 5)), four runs of four consecutive
-// features: the epilogue writes them with ds_write_b128 (layer_store).  The A
-// and B fragment layouts of 32x32 MFMAs are the same, so only the operand
-// order changes.
-template <int MR, int NR, bool TR>
+// The 4 K steps of one group: C layout, a lane owns column lane & 31 of every
+// tile, rows (q & 3) + 8 (q >> 2) + 4 (lane >> 5) (layer_store_c).
+template <int MR, int NR>
 __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[MR][NR]) {
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -210,8 +206,7 @@ __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[M
     for (int j = 0; j < NR; ++j) {
 #pragma unroll
       for (int m = 0; m < MR; ++m)
-        acc[m][j] = TR ? __builtin_amdgcn_mfma_f32_32x32x2f32(f.b[j][s], f.a[m][s], acc[m][j], 0, 0, 0)
-                       : __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[m][s], f.b[j][s], acc[m][j], 0, 0, 0);
+        acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[m][s], f.b[j][s], acc[m][j], 0, 0, 0);
     }
   }
 }
@@ -229,44 +224,17 @@ __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[M
 #endif
 constexpr int kRing = IKHIP_ANN_RING;
 
-// The accumulators of a transposed (TR) layer start at the bias of their
-// features, times `scale` (the fp16x3 weight pre-scale, undone with the
-// products); Keras adds it after the dot product (ann.py:46-56), a change of
-// summation order within the fp32 tolerance.
 template <int MR, int NR>
-__device__ __forceinline__ void acc_init_bias(f32x16 (&acc)[MR][NR], const float *bias, int nt0,
-                                              int nt_stride, int lane, float scale = 1.0f) {
-  const int h = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const float *b = bias + (nt0 + nt_stride * j) * 32 + 4 * h;
-    f32x16 v;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const f32x4 q = *reinterpret_cast<const f32x4 *>(b + 8 * i) * scale;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) v[4 * i + t] = q[t];
-    }
-#pragma unroll
-    for (int m = 0; m < MR; ++m) acc[m][j] = v;
-  }
-}
-
-template <int MR, int NR, bool TR>
 __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restrict__ wp, int G,
                                            int wbytes, int g0, int g1, int nt0, int nt_stride,
-                                           int lane, const float *bias, f32x16 (&acc)[MR][NR],
+                                           int lane, f32x16 (&acc)[MR][NR],
                                            unsigned long long *st_first = nullptr) {
   const int r = lane & 31, h = lane >> 5;
   const float *ap = H + r * kLd + 4 * h;
-  if (TR) {
-    acc_init_bias(acc, bias, nt0, nt_stride, lane);
-  } else {
 #pragma unroll
-    for (int j = 0; j < NR; ++j)
+  for (int j = 0; j < NR; ++j)
 #pragma unroll
-      for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
-  }
+    for (int m = 0; m < MR; ++m) acc[m][j] = (f32x16)(0.0f);
   if (g1 <= g0) return;
   Frag<MR, NR> f[kRing];
   const WStream<NR> ws = make_wstream<NR>(wp, wbytes, nt0, nt_stride, G, lane);
@@ -296,14 +264,14 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
       load_a(f[(u + kRing - 1) % kRing], a0, u);
       load_b(f[(u + kRing - 1) % kRing], g + kRing - 1, u);
       __builtin_amdgcn_sched_barrier(0);
-      mma_group<MR, NR, TR>(f[u], acc);
+      mma_group<MR, NR>(f[u], acc);
       __builtin_amdgcn_sched_barrier(0);
       if (u == 0 && g == g0) stamp(st_first);  // diagnostic: first K group done
     }
   }
 #pragma unroll
   for (int u = 0; u < kRing - 1; ++u)
-    if (g + u < g1) mma_group<MR, NR, TR>(f[u], acc);
+    if (g + u < g1) mma_group<MR, NR>(f[u], acc);
 }
 
 // fp16x3 activation planes.  A layer whose successor runs in fp16x3 stores its
@@ -319,7 +287,7 @@ __device__ __forceinline__ _Float16 *hplane(float *H, int row) {
   return reinterpret_cast<_Float16 *>(H + row * kLd);
 }
 
-// Plane swizzle (IKHIP_ANN_HSWZ): rows 4..11 of every 16 hold their 16-byte k-blocks
+// Plane swizzle: rows 4..11 of every 16 hold their 16-byte k-blocks
 // pairwise swapped (half index col ^ 8).  The 16x16x32 loop's ds_read_b128 of a K step
 // (lane: row lane & 15, k-block lane >> 4; kLd = 516 floats puts row r one 16-byte slot
 // after row r - 1) then lands each of the instruction's four 16-lane bank groups on 16
@@ -328,12 +296,7 @@ __device__ __forceinline__ _Float16 *hplane(float *H, int row) {
 // SQ_LDS_IDX_ACTIVE in the r04 fp16x3 profile).  Writers (store_h4 / store_h1) and
 // readers apply the same XOR; it touches only bit 3 of the half index, so K-step and
 // row-group offsets (multiples of 16 halves / 16 rows) pass through unchanged.
-#ifndef IKHIP_ANN_HSWZ
-#define IKHIP_ANN_HSWZ 1
-#endif
-__device__ __forceinline__ int hswz(int row) {
-  return IKHIP_ANN_HSWZ ? (((row + 4) >> 3) & 1) << 3 : 0;
-}
+__device__ __forceinline__ int hswz(int row) { return (((row + 4) >> 3) & 1) << 3; }
 
 __device__ __forceinline__ void store_h4(float *H, int row, int col, f32x4 v) {
   const f32x2 v01 = {v[0], v[1]}, v23 = {v[2], v[3]};
@@ -393,51 +356,15 @@ __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], i
   }
 }
 
-// Epilogue of a full-width split-mode layer on the transposed tile (mma_group TR): the
-// lane's point is row m * 32 + (lane & 31) of H, its 16 features four runs of
-// four at columns 32 nt + 8 i + 4 (lane >> 5), each one ds_write_b128; the bias
-// is already in the accumulators.  The activation runs on 8 elements at a
-// time, phase by phase, so the dependent exp / rcp chains of different
-// elements overlap (one element pair at a time, each step waiting on the last,
-// cost ~100 cycles per pair).  bf16x6 / fp16x3: 2-3 % faster than the C layout.
-template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
-__device__ __forceinline__ void layer_store(float *H, int wave, int lane, f32x16 (&acc)[MR][NR],
-                                            unsigned long long *st) {
-  const int r = lane & 31, h = lane >> 5;
-  stamp(st);
-  __syncthreads();  // every wave has finished reading the layer input
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    const int col0 = (wave + W * j) * 32 + 4 * h;
-#pragma unroll
-    for (int m = 0; m < MR; ++m) {
-      float *row = H + (m * 32 + r) * kLd + col0;
-#pragma unroll
-      for (int q0 = 0; q0 < 16; q0 += 8) {
-        f32x2 t[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) t[k] = f32x2{acc[m][j][q0 + 2 * k], acc[m][j][q0 + 2 * k + 1]};
-        act_apply2x4<ACT>(t);
-        if constexpr (HOUT) {
-          store_h4(H, m * 32 + r, col0 + 2 * q0, f32x4{t[0].x, t[0].y, t[1].x, t[1].y});
-          store_h4(H, m * 32 + r, col0 + 2 * q0 + 8, f32x4{t[2].x, t[2].y, t[3].x, t[3].y});
-        } else {
-          *reinterpret_cast<f32x4 *>(row + 2 * q0) = f32x4{t[0].x, t[0].y, t[1].x, t[1].y};
-          *reinterpret_cast<f32x4 *>(row + 2 * q0 + 8) = f32x4{t[2].x, t[2].y, t[3].x, t[3].y};
-        }
-      }
-    }
-  }
-}
-
 // ------------------------------------------------ split-bf16 (bf16x6) mode ----
 // Opt-in (IK_ANN_MODE_BF16X6): fp32 operands are split into three bf16 parts,
 // x = hi + mid + lo (each residual exact in fp32), and the six products whose
 // order is above 2^-24 -- lo*hi, mid*mid, hi*lo, mid*hi, hi*mid, hi*hi -- are
-// accumulated in fp32 by v_mfma_f32_32x32x16_bf16 (exact bf16 products).  The
-// result is fp32-accurate (max |d| vs a float64 forward ~1e-7 on the reference
-// architecture, tests/test_gpu_parity.py) at 6 bf16 MFMAs (192 cycles) per
-// 32x32x16 block instead of 8 fp32 ones (512 cycles).  Weights are split on
+// accumulated in fp32 by v_mfma_f32_16x16x32_bf16 (exact bf16 products;
+// layer_gemm_x16 below).  The result is fp32-accurate (max |d| vs a float64
+// forward ~1e-7 on the reference architecture, tests/test_gpu_parity.py) at 6
+// bf16 MFMAs per 32x32x16 block of work instead of 8 fp32 ones (192 against 512
+// cycles).  Weights are split on
 // the host into three fragment-ordered planes; activations are split in VALU
 // as they are read from LDS, in the MFMA issue gaps.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -473,108 +400,6 @@ __device__ __forceinline__ Split3 split3(f32x8 x) {
   return s;
 }
 
-// The weight planes of one 16-deep K step for the wave's NR column tiles
-// (plane p of step g of column tile nt: block (nt * G16 + g) * 3 + p of 64 lanes x 16 B).
-template <int NR>
-struct WStep {
-  bf16x8 p[NR][3];
-};
-
-template <int NR>
-__device__ __forceinline__ void load_w(WStep<NR> &w, const WStream<NR> &ws, int g) {
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int p = 0; p < 3; ++p) w.p[j][p] = wload<bf16x8>(ws, j, g * 3 + p);
-}
-
-// A fragments of K step g (lane: row lane&31, k 16g + 8*(lane>>5) + 0..7), two ds_read_b128.
-template <int MR>
-__device__ __forceinline__ void load_a(f32x8 (&a)[MR], const float *ap, int g) {
-#pragma unroll
-  for (int m = 0; m < MR; ++m) {
-    const f32x4 *q = reinterpret_cast<const f32x4 *>(ap + m * 32 * kLd + 16 * g);
-    const f32x4 lo4 = q[0], hi4 = q[1];
-    a[m] = f32x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
-  }
-}
-
-// One K step: the 6 * MR * NR MFMAs of step g (A already split, in sa) with the
-// operand traffic of later steps in their shadow -- the weight planes of step
-// g+2 (into the buffer step g-1 used: three buffers in flight, two steps of
-// L2 latency covered) and A of step g+1, read from LDS and split in VALU
-// between the MFMAs (sched_group_barrier pattern below), into sa for the next step.
-template <int MR, int NR, int GI>
-__device__ __forceinline__ void step_x(Split3 (&sa)[MR], const WStep<NR> &w, WStep<NR> &fill,
-                                       const WStream<NR> &ws, const float *ab, int g,
-                                       f32x16 (&acc)[MR][NR]) {
-  __builtin_amdgcn_sched_barrier(0);
-  load_w(fill, ws, g + 2);
-  f32x8 an[MR];
-  load_a(an, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
-  Split3 sn[MR];
-#pragma unroll
-  for (int m = 0; m < MR; ++m) sn[m] = split3(an[m]);
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      f32x16 c = acc[m][j];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][0], sa[m].lo, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][1], sa[m].mid, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][2], sa[m].hi, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][0], sa[m].mid, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][1], sa[m].hi, c, 0, 0, 0);
-      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w.p[j][0], sa[m].hi, c, 0, 0, 0);
-    }
-  // issue order: the loads, a few MFMAs to cover the LDS latency, then the
-  // split VALU two instructions per MFMA gap
-  constexpr int kMfma = 6 * MR * NR, kLead = (kMfma >= 12) ? 6 : kMfma / 2;
-  __builtin_amdgcn_sched_group_barrier(0x020, 3 * NR, 0);  // VMEM reads
-  __builtin_amdgcn_sched_group_barrier(0x100, 2 * MR, 0);  // DS reads
-  __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
-#pragma unroll
-  for (int i = 0; i < kMfma - kLead; ++i) {
-    __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-  }
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int m = 0; m < MR; ++m) sa[m] = sn[m];
-}
-
-// Full-width layer in bf16x6 mode (NR column tiles per wave).  A reads of the
-// step after the last run into the next row or H's pad, never multiplied.
-template <int MR, int NR, int W = kWaves>
-__device__ __forceinline__ void layer_gemm_x(const float *H, const bf16x8 *__restrict__ wx,
-                                             int G16, int xbytes, int wave, int lane,
-                                             const float *bias, f32x16 (&acc)[MR][NR]) {
-  const int r = lane & 31, h = lane >> 5;
-  const float *ap = H + r * kLd + 8 * h;
-  acc_init_bias(acc, bias, wave, W, lane);
-  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G16 * 3, lane);
-  WStep<NR> w0, w1, w2;
-  load_w(w0, ws, 0);
-  load_w(w1, ws, 1);
-  Split3 sa[MR];
-  {
-    f32x8 a0[MR];
-    load_a(a0, ap, 0);
-#pragma unroll
-    for (int m = 0; m < MR; ++m) sa[m] = split3(a0[m]);
-  }
-  int g = 0;
-  for (; g + 3 <= G16; g += 3) {
-    const float *ab = ap + 16 * g;
-    step_x<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
-    step_x<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
-    step_x<MR, NR, 2>(sa, w2, w1, ws, ab, g + 2, acc);
-  }
-  const float *ab = ap + 16 * g;
-  if (g < G16) step_x<MR, NR, 0>(sa, w0, w2, ws, ab, g, acc);
-  if (g + 1 < G16) step_x<MR, NR, 1>(sa, w1, w0, ws, ab, g + 1, acc);
-}
-
 // Compile-time loop: f(std::integral_constant<int, 0>) .. f(<N - 1>).
 template <int I, int N, typename F>
 __device__ __forceinline__ void static_for_(F &&f) {
@@ -592,9 +417,7 @@ __device__ __forceinline__ void static_for(F &&f) {
 // Opt-in (IK_ANN_FP16X3): x = hi + lo in fp16 (round to nearest; the residual
 // is exact in fp32), weights pre-scaled by 2^k so their largest is ~2^14, and
 // the three products above 2^-22 -- lo*hi, hi*lo, hi*hi -- accumulated in fp32
-// by v_mfma_f32_16x16x32_f16 (layer_gemm_h16, the default) or
-// v_mfma_f32_32x32x16_f16 (layer_gemm_h, IKHIP_ANN_H16=0); fp16 products are
-// exact in fp32.  The result is scaled back by 2^-k (exact).  3 MFMAs (96
+// by v_mfma_f32_16x16x32_f16 (layer_gemm_h16); fp16 products are exact in fp32.  The result is scaled back by 2^-k (exact).  3 MFMAs (96
 // cycles) per 32x32x16 block against 6 for bf16x6 and 8 fp32 ones (512
 // cycles), 4 B per weight from L2.  Only for
 // layers whose input is bounded (the layer before is tanh or sigmoid): fp16's
@@ -606,134 +429,20 @@ struct Split2 {
   f16x8 hi, lo;
 };
 
-
-// weight planes of one K step: plane p (0 hi, 1 lo) of step g of column tile
-// nt is block (nt * G16 + g) * 2 + p of 64 lanes x 16 B
-template <int NR>
-struct WStepH {
-  f16x8 p[NR][2];
-};
-
-template <int NR>
-__device__ __forceinline__ void load_wh(WStepH<NR> &w, const WStream<NR> &ws, int g) {
-#pragma unroll
-  for (int j = 0; j < NR; ++j)
-#pragma unroll
-    for (int p = 0; p < 2; ++p) w.p[j][p] = wload<f16x8>(ws, j, g * 2 + p);
-}
-
-// One K step (see step_x): weights of step g+2 and A of step g+1 in the shadow
-// of the 3 * MR * NR MFMAs of step g.
-#ifndef IKHIP_ANN_XRING
-#define IKHIP_ANN_XRING 3
-#endif
-// fp16x3 weight-step buffers (kXRing - 1 steps ahead).  4, 5 and 6 buffers
-// (no spills; AGPRs 136 -> 232) measured 15.66 / 15.84 / 15.77 ms against 15.50
-// for 3 at 1M points (tools/ann_ab.sh): the weight stream is not latency-bound
-// but at the L2's rate for a table every CU reads (DESIGN.md "fp16x3").
-constexpr int kXRing = IKHIP_ANN_XRING;
-// A fragments of K step g from the split planes (store_h4 / store_h1): lane: row
-// lane & 31, k 16g + 8 (lane >> 5) + 0..7, one ds_read_b128 per plane.
-template <int MR>
-__device__ __forceinline__ void load_ah(Split2 (&a)[MR], const _Float16 *ap, int g) {
-#pragma unroll
-  for (int m = 0; m < MR; ++m) {
-    const _Float16 *q = ap + m * 32 * 2 * kLd + 16 * g;
-    a[m].hi = *reinterpret_cast<const f16x8 *>(q);
-    a[m].lo = *reinterpret_cast<const f16x8 *>(q + 512);
-  }
-}
-
-template <int MR, int NR, int GI>
-__device__ __forceinline__ void step_h(Split2 (&sa)[MR], const WStepH<NR> &w, WStepH<NR> &fill,
-                                       const WStream<NR> &ws, const _Float16 *ab, int g,
-                                       f32x16 (&acc)[MR][NR]) {
-  __builtin_amdgcn_sched_barrier(0);
-  load_wh(fill, ws, g + kXRing - 1);
-  Split2 sn[MR];
-  load_ah(sn, ab, GI + 1);  // step g + 1; ab is the pass base (step g - GI)
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      f32x16 c = acc[m][j];
-      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][0], sa[m].lo, c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][1], sa[m].hi, c, 0, 0, 0);
-      acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(w.p[j][0], sa[m].hi, c, 0, 0, 0);
-    }
-  // (no in-loop VALU left to interleave: with the split planes the compiler's own
-  // order of the loads and MFMAs measured 1.6 % faster than the bf16x6 pattern)
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int m = 0; m < MR; ++m) sa[m] = sn[m];
-}
-
-// Full-width layer in fp16x3 mode; the accumulators come back scaled by xinv.
-template <int MR, int NR, int W = kWaves>
-__device__ __forceinline__ void layer_gemm_h(const float *H, const f16x8 *__restrict__ wx,
-                                             int G16, int xbytes, float xinv, int wave, int lane,
-                                             const float *bias, f32x16 (&acc)[MR][NR]) {
-  const int r = lane & 31, h = lane >> 5;
-  const _Float16 *ap = hplane(const_cast<float *>(H), r) + ((8 * h) ^ hswz(r));  // the split planes
-  acc_init_bias(acc, bias, wave, W, lane, 1.0f / xinv);  // exact: xinv is 2^-k
-  const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G16 * 2, lane);
-  WStepH<NR> w[kXRing];
-#pragma unroll
-  for (int u = 0; u < kXRing - 1; ++u) load_wh(w[u], ws, u);
-  Split2 sa[MR];
-  load_ah(sa, ap, 0);
-  int g = 0;
-  for (; g + kXRing <= G16; g += kXRing) {
-    const _Float16 *ab = ap + 16 * g;
-    static_for<kXRing>([&](auto u) {
-      step_h<MR, NR, u.value>(sa, w[u.value], w[(u.value + kXRing - 1) % kXRing], ws, ab,
-                              g + u.value, acc);
-    });
-  }
-  const _Float16 *ab = ap + 16 * g;
-  static_for<kXRing - 1>([&](auto u) {
-    if (g + u.value < G16)
-      step_h<MR, NR, u.value>(sa, w[u.value], w[(u.value + kXRing - 1) % kXRing], ws, ab,
-                              g + u.value, acc);
-  });
-#pragma unroll
-  for (int m = 0; m < MR; ++m)
-#pragma unroll
-    for (int j = 0; j < NR; ++j) acc[m][j] *= xinv;
-}
-
-// fp16x3 on v_mfma_f32_16x16x32_f16 (IKHIP_ANN_H16, the default).  Same
-// products, same cycles per FLOP as the 32x32x16 form above, but the chip holds
-// a higher clock under the power cap on the 16x16 shape (MI355X_MICROARCH.md,
-// "Shape").  A wave's 32x32 tile (m, j) is four 16x16 sub-tiles s = 2 fh + ph
+// fp16x3 on v_mfma_f32_16x16x32_f16.  The same products and cycles per FLOP as
+// the 32x32x16 shape (r01-r03's loop, history §3), but the chip holds a higher
+// clock under the power cap on the 16x16 shape (MI355X_MICROARCH.md, "Shape").  A wave's 32x32 tile (m, j) is four 16x16 sub-tiles s = 2 fh + ph
 // (feature half fh, point half ph), each in elements [4s, 4s + 4) of the f32x16
 // accumulator: lane l holds point 16 ph + (l & 15), features 32 nt + 16 fh +
 // 4 (l >> 4) + 0..3.  One K step is 32 deep: weights of plane p, feature half
 // fh at block ((g * 2 + fh) * 2 + p) of the tile (ann_pack_layer_h), and the
 // activations one ds_read_b128 per plane and point half.
-#ifndef IKHIP_ANN_H16
-#define IKHIP_ANN_H16 1
-#endif
-constexpr bool kH16 = IKHIP_ANN_H16 != 0;
-#ifndef IKHIP_ANN_BIAS_FIRST
-#define IKHIP_ANN_BIAS_FIRST 1
-#endif
 // weight-step buffers of the 16x16x32 loop (kH16Ring - 1 steps of 32 ahead)
 #ifndef IKHIP_ANN_H16_RING
 #define IKHIP_ANN_H16_RING 2
 #endif
 constexpr int kH16Ring = IKHIP_ANN_H16_RING;
-// 2: loads spread over the step's MFMAs (with 4 waves: 13.49 ms against 13.65 for
-// 8 waves in the compiler's order, 13.82 for 4 waves in it; 1 = loads first: 13.88)
-#ifndef IKHIP_ANN_H16_PATTERN
-#define IKHIP_ANN_H16_PATTERN 2
-#endif
 
-// IKHIP_EXP_L1W (timing experiment, wrong results): every step reads step 0's
-// blocks, which stay in L1 -- the weight stream without its L2 traffic.
-#ifndef IKHIP_EXP_L1W
-#define IKHIP_EXP_L1W 0
-#endif
 template <int NR>
 struct WStepH16 {
   f16x8 p[NR][2][2];  // [tile][feature half][plane]
@@ -747,7 +456,7 @@ __device__ __forceinline__ void load_wh16(WStepH16<NR> &w, const WStream<NR> &ws
     for (int fh = 0; fh < 2; ++fh)
 #pragma unroll
       for (int p = 0; p < 2; ++p)
-        w.p[j][fh][p] = wload<f16x8>(ws, j, (IKHIP_EXP_L1W ? 0 : g * 4) + fh * 2 + p);
+        w.p[j][fh][p] = wload<f16x8>(ws, j, g * 4 + fh * 2 + p);
 }
 
 // lane l: point 16 ph + (l & 15) of row group m, k 32 g + 8 (l >> 4) + 0..7
@@ -785,12 +494,9 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
           acc[m][j][2 * fh + ph] =
               __builtin_amdgcn_mfma_f32_16x16x32_f16(w.p[j][fh][0], sa[m][ph].hi, c, 0, 0, 0);
         }
-#if IKHIP_ANN_H16_PATTERN == 1
-  __builtin_amdgcn_sched_group_barrier(0x020, 4 * NR, 0);       // VMEM reads
-  __builtin_amdgcn_sched_group_barrier(0x100, 4 * MR, 0);       // DS reads
-  __builtin_amdgcn_sched_group_barrier(0x008, 12 * MR * NR, 0);  // MFMA
-#elif IKHIP_ANN_H16_PATTERN == 2
-  // one weight load, one LDS read per two MFMAs from the start of the step
+  // one weight load, one LDS read per two MFMAs from the start of the step (with
+  // 4 waves: 13.49 ms against 13.65 for 8 waves in the compiler's order, 13.82 for
+  // 4 waves in it, 13.88 with the loads first)
 #pragma unroll
   for (int i = 0; i < 4 * NR; ++i) {
     __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
@@ -798,7 +504,6 @@ __device__ __forceinline__ void step_h16(Split2 (&sa)[MR][2], const WStepH16<NR>
     if (i < 4 * MR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
   }
-#endif
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int m = 0; m < MR; ++m)
@@ -816,7 +521,7 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
   // the bias loads go out before the first weight step's: vmcnt counts in issue
   // order, so the accumulators' start (bias x scale) then waits for the bias
   // alone and the first MFMAs for their own weight blocks, not for all of the
-  // step's (IKHIP_ANN_BIAS_FIRST)
+  // step's
   f32x4 bl[NR][2];
 #pragma unroll
   for (int j = 0; j < NR; ++j)
@@ -824,7 +529,7 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
     for (int fh = 0; fh < 2; ++fh)
       bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
                                                    4 * (lane >> 4));
-  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 4, lane);
   WStepH16<NR> w[kH16Ring];
 #pragma unroll
@@ -901,21 +606,14 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
     }
 }
 
-// bf16x6 on v_mfma_f32_16x16x32_bf16 (IKHIP_ANN_X16): the same six products in
+// bf16x6 on v_mfma_f32_16x16x32_bf16: the same six products in
 // the 16x16 sub-tile layout of layer_gemm_h16 (epilogue layer_store_h16), the
 // activations split in VALU as they are read: lane l reads point 16 ph + (l & 15)
 // of row group m, k 32 g + 8 (l >> 4) + 0..7 (two ds_read_b128).  Weights: plane p
 // of feature half fh at block ((g * 2 + fh) * 3 + p) of the tile (ann_pack_layer_x).
 // Same box: 26.26 -> 24.12 ms per 1M points with the loads first (pattern 1, 40
 // VGPRs spilled outside the loop); 25.18 in the compiler's order (0, no spills);
-// weight loads spread (2): 23.5 against 23.1 for 1 on another box.
-#ifndef IKHIP_ANN_X16
-#define IKHIP_ANN_X16 1
-#endif
-constexpr bool kX16 = IKHIP_ANN_X16 != 0;
-#ifndef IKHIP_ANN_X16_PATTERN
-#define IKHIP_ANN_X16_PATTERN 1
-#endif
+// weight loads spread: 23.5 against 23.1 with them first on another box.
 
 template <int NR>
 struct WStepX16 {
@@ -975,22 +673,17 @@ __device__ __forceinline__ void step_x16(Split3 (&sa)[MR][2], const WStepX16<NR>
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[1], x.hi, c, 0, 0, 0);
           acc[m][j][2 * fh + ph] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wp[0], x.hi, c, 0, 0, 0);
         }
-#if IKHIP_ANN_X16_PATTERN
   // the loads, a few MFMAs to cover the LDS latency, then the split VALU two
-  // instructions per MFMA gap (as step_x)
+  // instructions per MFMA gap
   constexpr int kMfma = 24 * MR * NR, kLead = 6;
-  if (IKHIP_ANN_X16_PATTERN == 1)
-    __builtin_amdgcn_sched_group_barrier(0x020, 6 * NR, 0);  // VMEM reads, all first
+  __builtin_amdgcn_sched_group_barrier(0x020, 6 * NR, 0);  // VMEM reads, all first
   __builtin_amdgcn_sched_group_barrier(0x100, 4 * MR, 0);  // DS reads
   __builtin_amdgcn_sched_group_barrier(0x008, kLead, 0);   // MFMA
 #pragma unroll
   for (int i = 0; i < kMfma - kLead; ++i) {
-    if (IKHIP_ANN_X16_PATTERN == 2 && i % 2 == 0 && i / 2 < 6 * NR)
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read, spread
     __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // VALU
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
   }
-#endif
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int m = 0; m < MR; ++m)
@@ -1010,7 +703,7 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
     for (int fh = 0; fh < 2; ++fh)
       bl[j][fh] = *reinterpret_cast<const f32x4 *>(bias + (wave + W * j) * 32 + 16 * fh +
                                                    4 * (lane >> 4));
-  if (IKHIP_ANN_BIAS_FIRST) __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_sched_barrier(0);
   const WStream<NR> ws = make_wstream<NR>(wx, xbytes, wave, W, G32 * 6, lane);
   WStepX16<NR> w[2];
   load_wx16(w[0], ws, 0);
@@ -1058,9 +751,7 @@ __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[N
                                           int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st, float pre) {
   if (tr) {
-    if constexpr ((X == 2 && kH16) || (X == 1 && kX16))
-      layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st, pre);
-    else layer_store<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st);
+    if constexpr (X != 0) layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st, pre);
   } else {
     layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
   }
@@ -1084,33 +775,25 @@ template <int MR, int NR, int X = 0, bool HX = false, int W = kWaves>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           unsigned long long *st_first,
-                                          const void *wx = nullptr, int G16 = 0,
+                                          const void *wx = nullptr, int G32 = 0,
                                           float xinv = 1.0f, bool hout = false) {
   f32x16 acc[MR][NR];
   const int NT = wbytes / (G * 1024);  // column tiles of the layer
   float bv[NR];
   const bool tr = X != 0 && wx;  // split GEMM: transposed tile, bias in the accumulators
   if (tr) {
-    if (X == 1) {
-      if constexpr (kX16)  // G16: 32-deep K steps here
-        layer_gemm_x16<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 6 * 1024,
-                                  wave, lane, bias, acc);
-      else
-        layer_gemm_x<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G16, NT * G16 * 3 * 1024,
+    if (X == 1)  // G32: 32-deep K steps
+      layer_gemm_x16<MR, NR, W>(H, static_cast<const bf16x8 *>(wx), G32, NT * G32 * 6 * 1024,
                                 wave, lane, bias, acc);
-    }
-    else if constexpr (kH16)  // G16: 32-deep K steps here
-      layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 4 * 1024,
-                                xinv, wave, lane, bias, acc, st_first);
     else
-      layer_gemm_h<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G16, NT * G16 * 2 * 1024,
-                              xinv, wave, lane, bias, acc);
+      layer_gemm_h16<MR, NR, W>(H, static_cast<const f16x8 *>(wx), G32, NT * G32 * 4 * 1024,
+                                xinv, wave, lane, bias, acc, st_first);
   } else {
 #pragma unroll
     for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + W * j) * 32 + (lane & 31)];
-    layer_gemm<MR, NR, false>(H, wp, G, wbytes, 0, G, wave, W, lane, nullptr, acc, st_first);
+    layer_gemm<MR, NR>(H, wp, G, wbytes, 0, G, wave, W, lane, acc, st_first);
   }
-  const float pre = (X == 2 && kH16 && tr) ? xinv : 1.0f;
+  const float pre = (X == 2 && tr) ? xinv : 1.0f;
   if (HX && hout) store_act<true, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
   else store_act<false, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
 }
@@ -1144,7 +827,7 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
   // further waves only join the barriers)
   const int ws = wave < 4 ? wave : 4;
   const int g0 = (G * ws) / 4, g1 = wave < 4 ? (G * (wave + 1)) / 4 : g0;
-  layer_gemm<MR, 1, false>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, nullptr, acc);
+  layer_gemm<MR, 1>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, acc);
   stamp(st);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
@@ -1181,18 +864,16 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 // (a.m.wx[l]) take the split GEMM; the others (input layer, split-K output
 // layer, fp16x3-ineligible layers) stay fp32.
 // Waves per workgroup: 4, one per SIMD (NR column tiles each, 4 at full width).
-// IKHIP_ANN_XWAVES for the fp16x3 kernel at 64-point tiles: 4 with the 16x16x32
-// loop (its loads spread over the MFMAs, pattern 2: 13.34 against 13.59 ms for 8),
-// 8 with the 32x32x16 loop (two per SIMD, NR = 2: one wave's weight loads and LDS
-// reads issue under the other's MFMAs).
+// IKHIP_ANN_XWAVES for the fp16x3 kernel at 64-point tiles: 4 (its loads spread
+// over the MFMAs: 13.34 against 13.59 ms for 8).
 #ifndef IKHIP_ANN_BWAVES  // bf16x6: 8 waves measured 27.5 vs 25.6 ms (27 VGPR spills)
 #define IKHIP_ANN_BWAVES 4
 #endif
 #ifndef IKHIP_ANN_FWAVES  // fp32 at 64-point tiles (IKHIP_ANN_MR=2): 8 waves 40.9 ms, 4 41.6, MR=1 40.2
 #define IKHIP_ANN_FWAVES 4
 #endif
-#ifndef IKHIP_ANN_XWAVES  // 8 for the 32x32x16 loop (IKHIP_ANN_H16=0), 4 for 16x16x32
-#define IKHIP_ANN_XWAVES (IKHIP_ANN_H16 ? 4 : 8)
+#ifndef IKHIP_ANN_XWAVES
+#define IKHIP_ANN_XWAVES 4
 #endif
 template <int MR, int X>
 constexpr int ann_waves() {
@@ -1202,21 +883,15 @@ constexpr int ann_waves() {
                                          : kWaves;
 }
 
-#ifndef IKHIP_ANN_DYN  // 1: tiles claimed from a counter after the first; 0: static stride
-#define IKHIP_ANN_DYN 1
-#endif
-// Where the claim is issued.  0: by thread 0 at the tile's start (r02-r03); its
-// returning atomic is older than wave 0's first weight loads, so vmcnt (counted
-// in issue order) makes wave 0's first weight wait of layer 0 wait for it too.
-// 1 (r04): by the workgroup's last wave after the tile's last GEMM, when that wave
-// has no memory wait left in the tile (point I/O is wave 0's), so the atomic's
-// latency hides under the output epilogue.  Same box, bit-identical: fp32
-// 39.44 -> 39.17 ms, HBM traffic 33.6 -> 23.2 GB per launch, L2 hit 80.7 -> 86.2 %
-// (the workgroups of an XCD stay closer in phase, sharing more weight lines);
-// fp16x3 even (profiles/r04/ab/ann_claim_late.txt).
-#ifndef IKHIP_ANN_CLAIM
-#define IKHIP_ANN_CLAIM 1
-#endif
+// Tiles after the first are claimed from a launch-wide counter (a static stride
+// ends on the slowest workgroup's share: 0.7 % slower, profiles/r04/ab/
+// ann_dyn_traffic.txt).  The claim is issued by the workgroup's last wave after
+// the tile's last GEMM, when that wave has no memory wait left in the tile (point
+// I/O is wave 0's), so the atomic's latency hides under the output epilogue.
+// Issued by thread 0 at the tile's start instead (r02-r03), its returning atomic
+// was older than wave 0's first weight loads and vmcnt (counted in issue order)
+// made them wait for it: same box, bit-identical, 39.44 -> 39.17 ms, HBM traffic
+// 33.6 -> 23.2 GB per launch, L2 hit 80.7 -> 86.2 % (profiles/r04/ab/ann_claim_late.txt).
 template <int MR, int X>
 __global__ __launch_bounds__((64 * ann_waves<MR, X>()), (MR == 2 || kWide) ? 1 : 2) void
 ann_fused_kernel(AnnArgs a) {
@@ -1232,22 +907,15 @@ ann_fused_kernel(AnnArgs a) {
   const int64_t ntiles = (a.n + BM - 1) / BM;
   double blk_max = 0.0, blk_sum = 0.0;  // FK round-trip error of this lane's points
 
-#if IKHIP_ANN_DYN
   // tiles after the first are claimed from a launch-wide counter (DevStats heads[0],
   // zeroed by the stats reset before every solve): a workgroup that runs faster
   // (an XCD at a higher clock, a CU whose partner workgroup has finished) takes more
-  // tiles, so the launch does not end on the slowest workgroup's static share.  The
-  // claim is issued at a tile's start and read after its last barrier; two slots,
-  // so thread 0's next claim never overwrites the one the others are still reading.
+  // tiles, so the launch does not end on the slowest workgroup's static share.  Two
+  // slots, so the next claim never overwrites the one the others are still reading.
   __shared__ long long next_tile[2];
   unsigned long long *const tile_ctr = &a.S->heads[0][0];
-#endif
   int64_t it_local = 0;  // this workgroup's tile counter
   for (int64_t tile = blockIdx.x; tile < ntiles; ++it_local) {
-#if IKHIP_ANN_DYN
-    if (IKHIP_ANN_CLAIM == 0 && tid == 0)
-      next_tile[it_local & 1] = (long long)atomicAdd(tile_ctr, 1ull) + (long long)gridDim.x;
-#endif
     const int64_t pt = tile * BM + tid;
     // diagnostic stamps (block 0, first tiles, lane 0 of each wave): slot 0 tile
     // start, 1 staged, 2+2l layer l GEMM done, 3+2l layer l done, 31 tile done
@@ -1299,19 +967,17 @@ ann_fused_kernel(AnnArgs a) {
         run_layer_splitk<MR, X == 2, W>(HL, wp, bias, act, G, wave, lane, tid, sl, hout);
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
-        // K steps of the split GEMM: 16 deep (bf16x6, 32x32x16 fp16x3), 32 (16x16x32)
-        const int G16 =
-            ((X == 2 && kH16) || (X == 1 && kX16)) ? (a.m.kp[l] + 31) >> 5 : (a.m.kp[l] + 15) >> 4;
+        const int G32 = (a.m.kp[l] + 31) >> 5;  // 32-deep K steps of the split GEMM
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout);
             break;
           case 3:
-            if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout);
+            if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout);
             break;
-          case 2: run_layer<MR, 2, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
-          case 1: run_layer<MR, 1, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G16, xinv, hout); break;
+          case 2: run_layer<MR, 2, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout); break;
+          case 1: run_layer<MR, 1, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout); break;
           default: __syncthreads(); break;
         }
       } else {
@@ -1337,10 +1003,8 @@ ann_fused_kernel(AnnArgs a) {
       __syncthreads();
       stamp(sl ? sl + 1 : nullptr);
     }
-#if IKHIP_ANN_DYN
-    if (IKHIP_ANN_CLAIM == 1 && tid == W * 64 - 64)
+    if (tid == W * 64 - 64)  // the last wave, after the tile's last GEMM
       next_tile[it_local & 1] = (long long)atomicAdd(tile_ctr, 1ull) + (long long)gridDim.x;
-#endif
     // ---- output: StandardScaler.inverse_transform (in-place fp32, fp64 ops) + FK
     if (tid < BM) {
       bool valid = pt < a.n;
@@ -1369,11 +1033,7 @@ ann_fused_kernel(AnnArgs a) {
     }
     __syncthreads();  // the next tile's staging overwrites H
     stamp(stp ? stp + kStampSlots - 1 : nullptr);
-#if IKHIP_ANN_DYN
     tile = (int64_t)next_tile[it_local & 1];
-#else
-    tile += gridDim.x;
-#endif
   }
   // per-block FK-error stats: one atomic pair per wave holding points, into its shard.
   // The whole wave reduces (lanes >= BM hold zeros): at MR = 1 the upper half of
@@ -1448,8 +1108,8 @@ void ann_pack_layer(const float *W, int k, int n, float *dst) {
 }
 
 size_t ann_x_bytes(int k, int n) {
-  int k16 = (k + (kX16 ? 31 : 15)) / (kX16 ? 32 : 16) * (kX16 ? 32 : 16), np = (n + 31) / 32 * 32;
-  return (size_t)k16 * np * 6;
+  const int k32 = (k + 31) / 32 * 32, np = (n + 31) / 32 * 32;
+  return (size_t)k32 * np * 6;
 }
 
 static uint16_t bf16_rne(float x) {
@@ -1468,59 +1128,40 @@ static float bf16_to_f32(uint16_t h) {
 }
 
 // The bf16x6 weight operand: three bf16 planes p (0 hi, 1 mid, 2 lo) of the B
-// fragment of v_mfma_f32_32x32x16_bf16 for K step g of column tile nt, element
-// j (0..7) of lane l being W[16g + 8*(l>>5) + j][32nt + (l&31)]:
-// dst[(((nt*G16 + g)*3 + p)*64 + l)*8 + j], split here by round-to-nearest-even
-// exactly as split3() splits the activations on the GPU.  (An fp32 layout split
-// in the kernel reads 4 B per weight instead of 6 but measured slower at
-// 64-point tiles: 30.5 vs 27.3 ms per 1M points, the VALU being the dearer.)
+// fragment of v_mfma_f32_16x16x32_bf16 for K step g (32 deep) of feature half fh
+// of column tile nt, element j (0..7) of lane l being
+// W[32g + 8*(l>>4) + j][32nt + 16fh + (l&15)]:
+// dst[((((nt*G32 + g)*2 + fh)*3 + p)*64 + l)*8 + j], split here by
+// round-to-nearest-even exactly as split3() splits the activations on the GPU.
+// (An fp32 layout split in the kernel reads 4 B per weight instead of 6 but
+// measured slower at 64-point tiles: 30.5 vs 27.3 ms per 1M points, the VALU
+// being the dearer.)
 void ann_pack_layer_x(const float *W, int k, int n, void *dst) {
-  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
-  int G16 = k16 / 16, NT = np / 32;
+  const int np = (n + 31) / 32 * 32, NT = np / 32, G32 = (k + 31) / 32;
   uint16_t *d16 = static_cast<uint16_t *>(dst);
-  if (kX16) {  // 16x16x32 order: dst[((((nt*G32 + g)*2 + fh)*3 + p)*64 + l)*8 + j]
-    const int G32 = (k + 31) / 32;
-    for (int nt = 0; nt < NT; ++nt)
-      for (int g = 0; g < G32; ++g)
-        for (int fh = 0; fh < 2; ++fh)
-          for (int lane = 0; lane < 64; ++lane)
-            for (int j = 0; j < 8; ++j) {
-              const int kk = 32 * g + 8 * (lane >> 4) + j;
-              const int c = nt * 32 + 16 * fh + (lane & 15);
-              const float x = (kk < k && c < n) ? W[(size_t)kk * n + c] : 0.0f;
-              const uint16_t h = bf16_rne(x);
-              const float r1 = x - bf16_to_f32(h);
-              const uint16_t m = bf16_rne(r1);
-              const float r2 = r1 - bf16_to_f32(m);
-              const size_t base =
-                  ((((size_t)nt * G32 + g) * 2 + fh) * 3) * 64 * 8 + (size_t)lane * 8 + j;
-              d16[base] = h;
-              d16[base + 64 * 8] = m;
-              d16[base + 2 * 64 * 8] = bf16_rne(r2);
-            }
-    return;
-  }
   for (int nt = 0; nt < NT; ++nt)
-    for (int g = 0; g < G16; ++g)
-      for (int lane = 0; lane < 64; ++lane)
-        for (int j = 0; j < 8; ++j) {
-          const int kk = 16 * g + 8 * (lane >> 5) + j;
-          const int c = nt * 32 + (lane & 31);
-          const float x = (kk < k && c < n) ? W[(size_t)kk * n + c] : 0.0f;
-          const uint16_t h = bf16_rne(x);
-          const float r1 = x - bf16_to_f32(h);
-          const uint16_t m = bf16_rne(r1);
-          const float r2 = r1 - bf16_to_f32(m);
-          const size_t base = (((size_t)nt * G16 + g) * 3) * 64 * 8 + (size_t)lane * 8 + j;
-          d16[base] = h;
-          d16[base + 64 * 8] = m;
-          d16[base + 2 * 64 * 8] = bf16_rne(r2);
-        }
+    for (int g = 0; g < G32; ++g)
+      for (int fh = 0; fh < 2; ++fh)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int kk = 32 * g + 8 * (lane >> 4) + j;
+            const int c = nt * 32 + 16 * fh + (lane & 15);
+            const float x = (kk < k && c < n) ? W[(size_t)kk * n + c] : 0.0f;
+            const uint16_t h = bf16_rne(x);
+            const float r1 = x - bf16_to_f32(h);
+            const uint16_t m = bf16_rne(r1);
+            const float r2 = r1 - bf16_to_f32(m);
+            const size_t base =
+                ((((size_t)nt * G32 + g) * 2 + fh) * 3) * 64 * 8 + (size_t)lane * 8 + j;
+            d16[base] = h;
+            d16[base + 64 * 8] = m;
+            d16[base + 2 * 64 * 8] = bf16_rne(r2);
+          }
 }
 
 size_t ann_h_bytes(int k, int n) {
-  int k16 = (k + (kH16 ? 31 : 15)) / (kH16 ? 32 : 16) * (kH16 ? 32 : 16), np = (n + 31) / 32 * 32;
-  return (size_t)k16 * np * 4;
+  const int k32 = (k + 31) / 32 * 32, np = (n + 31) / 32 * 32;
+  return (size_t)k32 * np * 4;
 }
 
 // The power of two that brings the layer's largest |weight| to [2^13, 2^14):
@@ -1537,50 +1178,28 @@ int ann_h_scale_exp(const float *W, int k, int n) {
 }
 
 // The fp16x3 weight operand: planes p (0 hi, 1 lo) of W * 2^scale_exp in the
-// B-fragment order of v_mfma_f32_32x32x16_f16 (the bf16x6 layout with two
-// planes): dst[(((nt*G16 + g)*2 + p)*64 + l)*8 + j] = plane p of
-// W[16g + 8*(l>>5) + j][32nt + (l&31)] * 2^scale_exp, each plane rounded to
-// nearest (the scaled weight and its residual are exact in fp32).
-// With IKHIP_ANN_H16 (v_mfma_f32_16x16x32_f16, 32-deep K steps):
+// B-fragment order of v_mfma_f32_16x16x32_f16 (32-deep K steps):
 // dst[((((nt*G32 + g)*2 + fh)*2 + p)*64 + l)*8 + j] = plane p of
-// W[32g + 8*(l>>4) + j][32nt + 16fh + (l&15)] * 2^scale_exp.
+// W[32g + 8*(l>>4) + j][32nt + 16fh + (l&15)] * 2^scale_exp, each plane rounded
+// to nearest (the scaled weight and its residual are exact in fp32).
 void ann_pack_layer_h(const float *W, int k, int n, int scale_exp, void *dst) {
-  int k16 = (k + 15) / 16 * 16, np = (n + 31) / 32 * 32;
-  int G16 = k16 / 16, NT = np / 32;
+  const int np = (n + 31) / 32 * 32, NT = np / 32, G32 = (k + 31) / 32;
   _Float16 *d = static_cast<_Float16 *>(dst);
-  if (kH16) {
-    const int G32 = (k + 31) / 32;
-    for (int nt = 0; nt < NT; ++nt)
-      for (int g = 0; g < G32; ++g)
-        for (int fh = 0; fh < 2; ++fh)
-          for (int lane = 0; lane < 64; ++lane)
-            for (int j = 0; j < 8; ++j) {
-              const int kk = 32 * g + 8 * (lane >> 4) + j;
-              const int c = nt * 32 + 16 * fh + (lane & 15);
-              const float x =
-                  (kk < k && c < n) ? std::ldexp(W[(size_t)kk * n + c], scale_exp) : 0.0f;
-              const _Float16 h = (_Float16)x;
-              const size_t base =
-                  ((((size_t)nt * G32 + g) * 2 + fh) * 2) * 64 * 8 + (size_t)lane * 8 + j;
-              d[base] = h;
-              d[base + 64 * 8] = (_Float16)(x - (float)h);
-            }
-    return;
-  }
   for (int nt = 0; nt < NT; ++nt)
-    for (int g = 0; g < G16; ++g)
-      for (int lane = 0; lane < 64; ++lane)
-        for (int j = 0; j < 8; ++j) {
-          const int kk = 16 * g + 8 * (lane >> 5) + j;
-          const int c = nt * 32 + (lane & 31);
-          const float x =
-              (kk < k && c < n) ? std::ldexp(W[(size_t)kk * n + c], scale_exp) : 0.0f;
-          const _Float16 h = (_Float16)x;
-          const _Float16 lo = (_Float16)(x - (float)h);
-          const size_t base = (((size_t)nt * G16 + g) * 2) * 64 * 8 + (size_t)lane * 8 + j;
-          d[base] = h;
-          d[base + 64 * 8] = lo;
-        }
+    for (int g = 0; g < G32; ++g)
+      for (int fh = 0; fh < 2; ++fh)
+        for (int lane = 0; lane < 64; ++lane)
+          for (int j = 0; j < 8; ++j) {
+            const int kk = 32 * g + 8 * (lane >> 4) + j;
+            const int c = nt * 32 + 16 * fh + (lane & 15);
+            const float x =
+                (kk < k && c < n) ? std::ldexp(W[(size_t)kk * n + c], scale_exp) : 0.0f;
+            const _Float16 h = (_Float16)x;
+            const size_t base =
+                ((((size_t)nt * G32 + g) * 2 + fh) * 2) * 64 * 8 + (size_t)lane * 8 + j;
+            d[base] = h;
+            d[base + 64 * 8] = (_Float16)(x - (float)h);
+          }
 }
 
 // Tile rows per workgroup: 32 * MR points.  fp32: MR = 1 (two 32-point

@@ -388,15 +388,12 @@ __device__ __forceinline__ void commit_point(const FabArgs &a, int64_t i, const 
 // and the whole wave then runs the general get_angles for the flagged lanes in
 // a pass of its own, so the general code's registers are never live beside the
 // fast path's.  has: the lane holds a point; st: its status so far.
-#ifndef IKHIP_FAB_FAST_ANGLES  // 0: the general get_angles for every point (A/B builds)
-#define IKHIP_FAB_FAST_ANGLES 1
-#endif
 template <class Joints>
 __device__ __forceinline__ void angles_step(bool has, Joints joints, int &st, double th[4]) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) th[k] = __builtin_nan("");
   bool redo = false, fast = false;
-  if (IKHIP_FAB_FAST_ANGLES && has && st == IK_OK) {
+  if (has && st == IK_OK) {
     d3 J[4];
     joints(J);
     int sf = IK_OK;
@@ -404,7 +401,6 @@ __device__ __forceinline__ void angles_step(bool has, Joints joints, int &st, do
     redo = !fast;
     if (fast) st = sf;
   }
-  if (!IKHIP_FAB_FAST_ANGLES && has && st == IK_OK) redo = true;  // (A/B build: general only)
   if (__any(redo)) {  // wave-uniform and rare: coincident joints, zero divisors, x = 0 or y = 0
     if (redo) {
       d3 J[4];
@@ -485,16 +481,10 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
 #define IKHIP_ORD_PPT 16
 #endif
 constexpr int kOrdPPT = IKHIP_ORD_PPT;  // points per thread of the classify / scatter blocks
-// 1: classify and scatter in one launch (fabrik_classify_scatter_kernel): the queue
-// lives in kOrdClasses per-class regions of n entries (perm[k * n + slot]), so a
-// block needs no global class totals before it places its points.  r04, rocprof over
-// the timed windows, same box (profiles/r04/ab/fabrik_fused_scatter.txt): the one
-// launch takes 17.8 us against 13.5 + 9.8, but its queue order inside a cost class
-// (block-major, ballot ranks) makes the iteration kernel 4 % slower at tol 1e-3
-// (0.340 against 0.327 ms; even at 1e-5), with the same learned table: off.
-#ifndef IKHIP_FAB_FUSED_SCATTER
-#define IKHIP_FAB_FUSED_SCATTER 0
-#endif
+// (r04: classify and scatter in one launch, the queue in per-class regions of n
+// entries: the launch takes 17.8 us against 13.5 + 9.8, but its queue order inside a
+// cost class makes the iteration kernel 4 % slower at tol 1e-3 with the same learned
+// table; dropped, profiles/r04/ab/fabrik_fused_scatter.txt)
 // (r04: spreading a block's class run over its slots -- slot r * 4099 mod run length --
 // so that a grab's points come from the whole block: iteration kernel +0.9 %, scatter
 // +3 us; profiles/r04/ab/fabrik_order_spread_dropped.txt)
@@ -639,71 +629,6 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
   }
 }
 
-// 1'. classify + scatter in one pass (IKHIP_FAB_FUSED_SCATTER).  Each point's cell
-// and class as in classify; a wave ranks its points of one class with four
-// ballots (the lanes whose class bits all agree) and one LDS atomic per class
-// present (one lane per class: no same-address serialization); the block then
-// reserves a run in each class region with one global atomic per class and writes
-// its points there.  The sampled points' cells go straight into the high halves of
-// their cost-table sample words (the retire step fills in the low halves).
-__global__ __launch_bounds__(256) void fabrik_classify_scatter_kernel(FabArgs a) {
-  __shared__ unsigned int cnt[kOrdClasses], base[kOrdClasses];
-  __shared__ uint8_t cls[kOrdCells];
-  const int t = threadIdx.x, lane = t & 63;
-  const int64_t b0 = (int64_t)blockIdx.x * (256 * kOrdPPT);
-  d3 g[kOrdPPT];
-#pragma unroll
-  for (int j = 0; j < kOrdPPT; ++j) {  // all loads in flight before the first use
-    const int64_t i = b0 + j * 256 + t;
-    if (i < a.n) g[j] = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
-  }
-  if (t < kOrdClasses) cnt[t] = 0;
-  static_assert(kOrdCells % 256 == 0, "whole table rows per thread");
-  unsigned int key[kOrdCells / 256];
-#pragma unroll
-  for (int q = 0; q < kOrdCells / 256; ++q) key[q] = a.ord->key[t + 256 * q];
-#pragma unroll
-  for (int q = 0; q < kOrdCells / 256; ++q)
-    cls[t + 256 * q] = (uint8_t)key_class(key[q], a.max_iter);
-  __syncthreads();
-  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  unsigned int loc[kOrdPPT];
-  int kk[kOrdPPT];
-#pragma unroll
-  for (int j = 0; j < kOrdPPT; ++j) {
-    const int64_t i = b0 + j * 256 + t;
-    const bool valid = i < a.n;
-    int k = 0;
-    if (valid) {
-      const int cell = goal_cell(a.r, g[j]);
-      k = cls[cell];
-      if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample)
-        reinterpret_cast<uint16_t *>(&a.ord->sample[i / kOrdSample])[1] = (uint16_t)cell;
-    }
-    unsigned long long peers = __ballot(valid);
-#pragma unroll
-    for (int bit = 0; bit < 4; ++bit) {
-      const bool on = (k >> bit) & 1;
-      const unsigned long long b = __ballot(on);
-      peers &= on ? b : ~b;
-    }
-    const int leader = __ffsll((long long)peers) - 1;
-    unsigned int r0 = 0;
-    if (valid && lane == leader) r0 = atomicAdd(&cnt[k], (unsigned int)__popcll(peers));
-    r0 = __shfl(r0, leader < 0 ? lane : leader, 64);
-    loc[j] = r0 + (unsigned int)__popcll(peers & lt);
-    kk[j] = k;
-  }
-  __syncthreads();
-  if (t < kOrdClasses) base[t] = cnt[t] ? atomicAdd(&a.S->cls_cur[t][0], cnt[t]) : 0u;
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kOrdPPT; ++j) {
-    const int64_t i = b0 + j * 256 + t;
-    if (i < a.n) a.perm[(int64_t)kk[j] * a.n + base[kk[j]] + loc[j]] = (int32_t)i;
-  }
-}
-
 // 3. persistent iteration with per-lane refill, seed and angles in batches.
 //
 // A lane whose point converged is refilled from the wave's batch of prepared
@@ -783,10 +708,7 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
     if constexpr (ORD) {
       if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample) {
         const uint32_t lo = (uint32_t)(it < 0xffff ? it : 0xffff);
-        if (IKHIP_FAB_FUSED_SCATTER)  // (the cell is already in the high half)
-          reinterpret_cast<uint16_t *>(&a.ord->sample[i / kOrdSample])[0] = (uint16_t)lo;
-        else
-          a.ord->sample[i / kOrdSample] = ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) | lo;
+        a.ord->sample[i / kOrdSample] = ((uint32_t)(a.cell[i] & (kOrdCells - 1)) << 16) | lo;
       }
     }
   }
@@ -803,22 +725,15 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 #ifndef IKHIP_FAB_REFILL  // free lanes that trigger a refill (r01: 8 against 4 / 16)
 #define IKHIP_FAB_REFILL 8
 #endif
-#ifndef IKHIP_FAB_INNER  // 1: the iterations in a loop of their own inside the refill loop
-#define IKHIP_FAB_INNER 1
-#endif
 #ifndef IKHIP_ITER_WAVES
 #define IKHIP_ITER_WAVES 2
 #endif
-// 1: the refill (park, stage, hand-out) at raised wave priority, like the seed and
+// The refill (park, stage, hand-out) runs at raised wave priority, like the seed and
 // angles steps: its dependent chains issue when ready instead of in the partner's
 // leftover slots.  r04, same box: iteration kernel -1.7 % at tol 1e-3, -1.3 % at 1e-5
 // (rocprof windows, 3 / 2 runs each), -1.0 / -1.3 % per bench step in another lease.
-#ifndef IKHIP_FAB_REFILL_PRIO
-#define IKHIP_FAB_REFILL_PRIO 1
-#endif
-#ifndef IKHIP_FAB_PREP_CARRY  // 1 (CORE 2): the seed's carried quotient taken in the prepare step
-#define IKHIP_FAB_PREP_CARRY 0
-#endif
+// (Taking the seed's carried quotient in the prepare step instead of at the
+// hand-out measured slower: profiles/r04/ab/fabrik_refill_prio_prep_carry.txt.)
 constexpr int kIterWaves = IKHIP_ITER_WAVES;  // waves per SIMD = blocks per CU
 template <int REFILL_MIN, bool ORD, int CORE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kIterWaves, kIterWaves))) void
@@ -840,10 +755,6 @@ fabrik_iter_kernel(FabArgs a) {
   struct PrepBatch {
     double v[12][64];  // seed joints 0..2 and the goal
     long long idx[64];
-#if IKHIP_FAB_PREP_CARRY
-    double c[4][64];   // CORE 2: the seed's carry (cq, cd), taken at full width
-    uint32_t cdom[64];
-#endif
   };
   __shared__ PrepBatch batches[4];
   PrepBatch &PB = batches[threadIdx.x >> 6];
@@ -857,10 +768,6 @@ fabrik_iter_kernel(FabArgs a) {
   // until that one runs dry; then the next one its block has not seen dry)
   __shared__ unsigned int dry_heads;  // the heads this block found dry
   if (threadIdx.x == 0) dry_heads = 0;
-  // IKHIP_FAB_FUSED_SCATTER: the class regions' fill, hardest class first
-  __shared__ unsigned int ctot[kOrdClasses];
-  if (IKHIP_FAB_FUSED_SCATTER && ORD && threadIdx.x < kOrdClasses)
-    ctot[threadIdx.x] = a.S->cls_cur[kOrdClasses - 1 - threadIdx.x][0];
   __syncthreads();
   int head = (int)(blockIdx.x % kQueueHeads);
   unsigned long long na = 0;
@@ -914,7 +821,7 @@ fabrik_iter_kernel(FabArgs a) {
     if (dry && nfree == 64) break;
     IKHIP_DG(kDiagLoops, 1);
     if (!dry && (nfree >= REFILL_MIN || nfree == 64)) {
-      if (IKHIP_FAB_REFILL_PRIO) prio_raise();
+      prio_raise();
       IKHIP_DG(kDiagRefills, 1);
       IKHIP_DT(kDiagTRefill);  // refill time, less the flushes and preparations in it
       IKHIP_DT(kDiagTSub);
@@ -926,7 +833,7 @@ fabrik_iter_kernel(FabArgs a) {
           IKHIP_DG(kDiagFlushes, 1);
           IKHIP_DT(kDiagTEnd);  // (scratch slot: the flush's start)
           ring_flush<ORD>(a, R, rcnt, lane, acc);
-          if (IKHIP_FAB_REFILL_PRIO) prio_raise();  // (the flush dropped it)
+          prio_raise();  // (the flush dropped it)
           IKHIP_DT_ACC(kDiagFlushTicks, kDiagTEnd);
           IKHIP_DT_ACC(kDiagTRefill, kDiagTEnd);  // (not refill time)
           rcnt = 0;
@@ -966,23 +873,7 @@ fabrik_iter_kernel(FabArgs a) {
         }
         ncount = (int)min((int64_t)a.chunk, a.n - nbase);
         if (lane < ncount) {
-          if (!ORD) {
-            nperm = nbase + lane;
-          } else if (IKHIP_FAB_FUSED_SCATTER) {
-            // queue position -> (class region, slot), hardest class first
-            int64_t q = nbase + lane;
-            int k = 0;
-#pragma unroll
-            for (int c = 0; c < kOrdClasses - 1; ++c) {
-              const int64_t tc = ctot[c];
-              const bool past = k == c && q >= tc;
-              q -= past ? tc : 0;
-              k += past ? 1 : 0;
-            }
-            nperm = (int64_t)a.perm[(int64_t)(kOrdClasses - 1 - k) * a.n + q];
-          } else {
-            nperm = (int64_t)a.perm[nbase + lane];
-          }
+          nperm = ORD ? (int64_t)a.perm[nbase + lane] : nbase + lane;
         }
         nstage = 2;
       };
@@ -1027,18 +918,7 @@ fabrik_iter_kernel(FabArgs a) {
             PB.v[6][lane] = Js[2].x; PB.v[7][lane] = Js[2].y; PB.v[8][lane] = Js[2].z;
             PB.v[9][lane] = ng.x; PB.v[10][lane] = ng.y; PB.v[11][lane] = ng.z;
             PB.idx[lane] = ni;
-#if IKHIP_FAB_PREP_CARRY
-            if constexpr (CORE == 2) {
-              double pq;
-              d3 pd;
-              uint32_t pdom;
-              reuse_carry(Js[2], ng, L[3], pq, pd, pdom);
-              PB.c[0][lane] = pq; PB.c[1][lane] = pd.x; PB.c[2][lane] = pd.y; PB.c[3][lane] = pd.z;
-              PB.cdom[lane] = pdom;
-            }
-#endif
           }
-          if (!IKHIP_FAB_REFILL_PRIO) prio_drop();
 #ifdef IKHIP_DIAG
           // (the seed's loads are consumed before the stamp)
           __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the batch's LDS writes landed
@@ -1061,30 +941,20 @@ fabrik_iter_kernel(FabArgs a) {
           ge = 1.0;
           step = 0;
           active = true;
-#if IKHIP_FAB_PREP_CARRY
-          if constexpr (CORE == 2) {
-            cq = PB.c[0][src];
-            cd = {PB.c[1][src], PB.c[2][src], PB.c[3][src]};
-            cdom = PB.cdom[src];
-          }
-#else
           if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
-#endif
         }
         pptr += take;
         handed += take;
       }
       dry = nstage < 0 && pptr >= pcount;
       IKHIP_DT_ACC(kDiagRefillTicks, kDiagTRefill);
-      if (IKHIP_FAB_REFILL_PRIO) prio_drop();
+      prio_drop();
     }
-#if IKHIP_FAB_INNER
     // iterate until a refill is due (REFILL_MIN lanes free) or, once the queue is
     // dry, until every lane has stopped: the refill's scalar state stays out of
     // this loop, so its SGPRs are not reloaded from their spill lanes per iteration
     const int need = dry ? 64 : REFILL_MIN;
     while (true) {
-#endif
 #ifdef IKHIP_DIAG
     {
       const unsigned long long sm =
@@ -1104,9 +974,7 @@ fabrik_iter_kernel(FabArgs a) {
       const bool run = active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step);
       pending = pending || (active && !run);
       active = run;
-#if IKHIP_FAB_INNER
       if (__popcll(__ballot(!run)) >= need) break;
-#endif
       if (run) {
         if constexpr (CORE == 2) {
           uint32_t dom = 0, cdom_n = cdom;
@@ -1147,9 +1015,7 @@ fabrik_iter_kernel(FabArgs a) {
         ++step;
       }
     }
-#if IKHIP_FAB_INNER
     }
-#endif
   }
   // drain: park the last finished lanes, then the angles step on the ring
   IKHIP_DT(kDiagTDrain);
@@ -1201,8 +1067,7 @@ __global__ __launch_bounds__(256) void fabrik_fold_kernel(FabArgs a) {
 static size_t up256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 size_t fabrik_scratch_bytes(int64_t n) {
-  // work order: perm n int32 (fused: kOrdClasses regions of n), cell n uint16 (unfused)
-  if (IKHIP_FAB_FUSED_SCATTER) return up256((size_t)n * 4 * kOrdClasses) + 1024;
+  // work order: perm n int32, cell n uint16
   return up256((size_t)n * 4) + up256((size_t)n * 2) + 1024;
 }
 
@@ -1281,20 +1146,14 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     char *p = static_cast<char *>(scratch);
     const unsigned ogrid = (unsigned)((n + 256 * kOrdPPT - 1) / (256 * kOrdPPT));
     a.perm = reinterpret_cast<int32_t *>(p);
-    if (IKHIP_FAB_FUSED_SCATTER) {
-      kt_begin("fabrik_classify_scatter_kernel", stream);
-      hipLaunchKernelGGL(fabrik_classify_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
-      kt_end(stream);
-    } else {
-      p += up256((size_t)n * 4);
-      a.cell = reinterpret_cast<uint16_t *>(p);
-      kt_begin("fabrik_classify_kernel", stream);
-      hipLaunchKernelGGL(fabrik_classify_kernel, dim3(ogrid), dim3(256), 0, stream, a);
-      kt_end(stream);
-      kt_begin("fabrik_scatter_kernel", stream);
-      hipLaunchKernelGGL(fabrik_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
-      kt_end(stream);
-    }
+    p += up256((size_t)n * 4);
+    a.cell = reinterpret_cast<uint16_t *>(p);
+    kt_begin("fabrik_classify_kernel", stream);
+    hipLaunchKernelGGL(fabrik_classify_kernel, dim3(ogrid), dim3(256), 0, stream, a);
+    kt_end(stream);
+    kt_begin("fabrik_scatter_kernel", stream);
+    hipLaunchKernelGGL(fabrik_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
+    kt_end(stream);
   }
   // persistent grid: blocks_per_cu 256-thread blocks per CU (= waves per SIMD)
   // measured on MI355X (tools/sweep_fabrik.py): at 1M points 2 blocks/CU with
