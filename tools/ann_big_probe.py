@@ -3,7 +3,7 @@ csrc/ik_ann_big.hip): a few model shapes on n random_dist points, device arrays,
 per-kernel HIP-event times of one call and the mean of `reps` calls; prints one JSON
 line per model with the achieved TFLOP/s of the Dense layers (2 * sum in * out per point).
 
-    python tools/ann_big_probe.py [n]
+    python tools/ann_big_probe.py [n] [only]   (only: e.g. 4096x2, one model)
 """
 import json
 import os
@@ -23,8 +23,11 @@ def main():
     ctx = _native.Context(0)
     pts = torch.from_numpy(random_dist(n, seed=0)).cuda()
     ang = torch.empty((n, 4), dtype=torch.float32, device="cuda")
+    only = sys.argv[2] if len(sys.argv) > 2 else None
     for dims in ((3, 2048, 2048, 4), (3,) + (512,) * 30 + (4,), (3, 4096, 4096, 4),
                  (3,) + (500,) * 12 + (4,)):
+        if only and only != f"{dims[1]}x{len(dims) - 2}":
+            continue
         m = glorot_model(dims=dims, seed=1)
         ctx.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
         flop = 2 * sum(dims[i] * dims[i + 1] for i in range(len(dims) - 1)) * n
