@@ -9,10 +9,9 @@
 //   annb_in_kernel     workspace check + StandardScaler.transform (float64) -> fp32
 //                      rows of 8 (x, y, z, 0...)
 //   annb_gemm_kernel   Y = act(X @ W + b), exact-fp32 v_mfma_f32_32x32x2_f32;
-//                      128 x 128 output tiles, 4 waves each 64 x 64, the X tile
-//                      double-buffered through LDS 32 deep in K, the weights read
-//                      straight from L2 in the fused kernel's packed fragment order
-//                      (ann_pack_layer: one 16-byte load per lane per 8-deep group)
+//                      256 x 128 output tiles, 8 waves each 64 x 64, the X tile and
+//                      the weights (the fused kernel's packed fragment order,
+//                      ann_pack_layer) double-buffered through LDS 32 deep in K
 //   annb_out_kernel    StandardScaler.inverse_transform (in-place fp32, float64
 //                      ops) + the cli.py:54-61 FK round trip + stats, as the fused
 //                      kernel's epilogue does
@@ -21,6 +20,7 @@
 // activation budget.  Still one library call (ik_ann_solve): the chunk loop is
 // host code on the context's stream.
 #include <cmath>
+#include <type_traits>
 
 #include "ik_common.h"
 
@@ -30,8 +30,7 @@ namespace annb {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kBM = 128;      // output rows per workgroup
-constexpr int kBN = 128;      // output columns per workgroup (4 column tiles of 32)
+constexpr int kBM = 128;      // chunk granularity of the activation buffers (rows)
 constexpr int kBK = 32;       // K per LDS stage (4 groups of 8)
 constexpr int kLdA = kBK + 4; // LDS row stride in floats (= 4 mod 32: conflict-free b128 reads)
 
@@ -77,127 +76,201 @@ __global__ __launch_bounds__(256) void annb_in_kernel(const double *__restrict__
 // permuted K order (4 consecutive activations per lane half), so each MFMA step
 // s pairs the same k on both operands.  Output columns past the layer's width
 // get act(0 + 0): finite, and the next layer's packed weights are zero there.
-__global__ __launch_bounds__(256) void annb_gemm_kernel(const float *__restrict__ A, int lda,
-                                                        int64_t rows,
-                                                        const f32x4 *__restrict__ wp, int G,
-                                                        int NT, const float *__restrict__ bias,
-                                                        int act, float *__restrict__ C,
-                                                        int ldc) {
-  __shared__ __attribute__((aligned(16))) float As[2][kBM * kLdA];
+//
+// Workgroup tile 128 rows x 128 columns, 4 waves (one per SIMD) of 64 x 64 (2 x 2
+// accumulators of v_mfma_f32_32x32x2_f32), two workgroups per CU so that one's
+// barrier and stage turnover run under the other's MFMAs; K in stages of 32 (4
+// groups of 8).  Both operands go through LDS, double-buffered: the stage's A tile
+// (128 x 32 floats, 18 KiB with the row pad, from HBM) and its B tile (the block's
+// 4 column tiles x 4 groups, 16 KiB of packed fragments, from L2 / MALL) are loaded
+// once per workgroup and read by the two waves that need each.  Both are loaded
+// two stages ahead into one of two register sets and written to the stage's
+// buffer at the start of the stage before (their loads are a stage old by then);
+// inside a stage the next group's fragments are read from LDS before the current
+// group's MFMAs are issued.  One barrier per stage.  (r04's kernel read B straight
+// from L2 in every wave and stored A after the MFMAs: 0.67-0.73 of the fp32 MFMA
+// peak, MFMA busy 76 %; 256 x 128 tiles, one workgroup per CU: the same.)
+// WN: waves along the columns (2: 2 x 2 waves of 64 x 64, 128 columns; 1: the
+// layer has a single column tile -- the 4-angle output layer -- and the 4 waves
+// take 32 rows x 32 columns each, so no wave multiplies 96 padding columns).
+constexpr int kBM2 = 128;  // output rows per workgroup
+template <int WN>
+__global__ __launch_bounds__(256, 2) void annb_gemm_kernel(const float *__restrict__ A, int lda,
+                                                           int64_t rows,
+                                                           const f32x4 *__restrict__ wp, int G,
+                                                           int NT, const float *__restrict__ bias,
+                                                           int act, float *__restrict__ C,
+                                                           int ldc) {
+  constexpr int WM = 4 / WN;          // waves along the rows
+  constexpr int MT = kBM2 / 32 / WM;  // 32-row tiles per wave
+  constexpr int JT = WN == 2 ? 2 : 1; // 32-column tiles per wave
+  constexpr int NTB = WN * JT;        // column tiles per workgroup
+  __shared__ __attribute__((aligned(16))) float As[2][kBM2 * kLdA];  // 2 x 18 KiB
+  __shared__ __attribute__((aligned(16))) f32x4 Bs[2][NTB * 4 * 64];  // 2 x NTB x 4 KiB
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so
-  // workgroup b runs on XCD b % 8; XCD x takes row panels x, x + 8, ... and every
-  // column block of a panel in turn, so a panel's A tile is read from HBM once into
-  // that XCD's L2 and reused by all its column blocks
-  const int nCB = (NT + kBN / 32 - 1) / (kBN / 32);
-  const unsigned b = blockIdx.x, xcd = b & 7u, k = b >> 3;
-  const int64_t rb = (int64_t)(k / (unsigned)nCB) * 8 + xcd;
-  const int cb = (int)(k % (unsigned)nCB);
-  if (rb * kBM >= rows) return;  // the grid's last panel row is padded to 8
-  const int64_t row0 = rb * kBM;
-  const int nt0 = cb * (kBN / 32) + wn * 2;  // this wave's two column tiles
+  const int wm = wave / WN, wn = wave % WN;
+  // XCD-aware tile order in 2-D groups: workgroups are dealt round-robin over the 8
+  // XCDs (workgroup b runs on XCD b % 8), and each XCD's consecutive workgroups --
+  // the ones resident together -- cover a group of BH row panels x BW column blocks
+  // (BW = 8, BH = 8 for layers of >= 1024 columns), so every stage's A tile is read
+  // into the XCD's L2 once for BW workgroups and every B tile once for BH of them.
+  // (Panel-major order, all column blocks of two panels at a time, re-read the
+  // weights from MALL for every panel pair: L2 hit 52 %.)
+  const int nCB = (NT + NTB - 1) / NTB;
+  const int64_t nRB = (rows + kBM2 - 1) / kBM2;
+  const int BW = nCB < 8 ? nCB : 8, BH = 64 / BW, per = BH * BW;
+  const int nBC = (nCB + BW - 1) / BW;
+  const unsigned b = blockIdx.x, xcd = b & 7u, kx = b >> 3;
+  const int64_t grp = (int64_t)(kx / (unsigned)per) * 8 + xcd;
+  const int inb = (int)(kx % (unsigned)per);
+  const int64_t rb = (grp / nBC) * BH + inb / BW;
+  const int cb = (int)(grp % nBC) * BW + inb % BW;
+  if (rb >= nRB || cb >= nCB) return;  // the grid is padded to whole groups
+  const int64_t row0 = rb * kBM2;
+  const int ntb = cb * NTB;  // the block's first column tile
   const int r = lane & 31, h = lane >> 5;
-  f32x16 acc[2][2];
+  f32x16 acc[MT][JT];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < MT; ++m)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[m][j] = (f32x16)(0.0f);
+    for (int j = 0; j < JT; ++j) acc[m][j] = (f32x16)(0.0f);
 
-  // the A tile of one stage: 128 rows x 32 floats, 4 x 16 bytes per thread, loaded
-  // two stages ahead into one of two register sets (the loads' HBM latency under
-  // load outlasts one stage of MFMAs) and written to the LDS buffer of its stage at
-  // the end of the stage before
+  // Operand loads through buffer descriptors, branch-free: a load past a
+  // descriptor's range returns zeros, so rows past the chunk, columns past the
+  // layer and K groups past the layer read 0 with no per-load branch (which made
+  // the compiler wait for every outstanding load before each LDS write, and copy
+  // the accumulators between the branches' register sets: 128 moves a stage).
+  // A: the panel's rows from row0 on; B: the block's column tiles from ntb on.
+  const uint32_t kOOB = 0x80000000u;  // an offset past any range below
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(A) + row0 * (int64_t)lda, 0,
+      (int)((rows - row0 < kBM2 ? rows - row0 : kBM2) * (int64_t)lda * 4), 0x00020000);
+  const auto rsB = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<f32x4 *>(wp) + (size_t)ntb * G * 64, 0,
+      (int)((NT - ntb < NTB ? NT - ntb : NTB) * G * 1024), 0x00020000);
   const int nst = (G + 3) / 4;
-  f32x4 ra0[4], ra1[4];
+  // A tile of stage s: 128 rows x 32 floats, 4 x 16 bytes per thread (row idx >> 3,
+  // columns 4 (idx & 7) ..), zero past the row's lda floats
   auto load_a = [&](f32x4 (&ra)[4], int s) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + 256 * i;
-      const int row = idx >> 3, c4 = idx & 7;
-      const int64_t gr = row0 + row;
-      const int kk = s * kBK + 4 * c4;
-      ra[i] = (s < nst && gr < rows && kk < lda)
-                  ? *reinterpret_cast<const f32x4 *>(A + gr * (int64_t)lda + kk)
-                  : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      const int kk = s * kBK + 4 * (idx & 7);
+      const uint32_t off = kk < lda ? (uint32_t)(((idx >> 3) * lda + kk) * 4) : kOOB;
+      ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
     }
   };
-  auto store_a = [&](const f32x4 (&ra)[4], int buf) {
+  // B tile of stage s: block (ntl, u) = the packed fragments of column tile ntb + ntl,
+  // group 4s + u; NTB x 16 bytes per thread, lane-linear in LDS
+  auto load_b = [&](f32x4 (&rbv)[NTB], int s) {
+#pragma unroll
+    for (int i = 0; i < NTB; ++i) {
+      const int idx = tid + 256 * i;
+      const int blk = idx >> 6, g = s * 4 + (blk & 3);
+      const uint32_t off = g < G ? (uint32_t)((((blk >> 2) * G + g) * 64 + (idx & 63)) * 16) : kOOB;
+      rbv[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsB, off, 0, 0));
+    }
+  };
+  auto store = [&](const f32x4 (&ra)[4], const f32x4 (&rbv)[NTB], int buf) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + 256 * i;
-      const int row = idx >> 3, c4 = idx & 7;
-      *reinterpret_cast<f32x4 *>(&As[buf][row * kLdA + 4 * c4]) = ra[i];
+      *reinterpret_cast<f32x4 *>(&As[buf][(idx >> 3) * kLdA + 4 * (idx & 7)]) = ra[i];
     }
-  };
-  // the weight fragments of stage s (zero for column tiles past the layer), loaded one
-  // stage ahead so that their L2 latency hides under the stage before's MFMAs
-  auto load_b = [&](f32x4 (&b)[4][2], int s) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int g = s * 4 + u, nt = nt0 + j;
-        b[u][j] = (g < G && nt < NT) ? wp[((size_t)nt * G + g) * 64 + lane]
-                                     : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      }
+    for (int i = 0; i < NTB; ++i) Bs[buf][tid + 256 * i] = rbv[i];
   };
-  // stage s: the next stage's weights and the A tile two ahead go out, the MFMAs of
-  // this stage run, then the A tile of stage s + 1 (loaded one stage ago) goes to LDS
-  auto stage = [&](int s, f32x4 (&bn)[4][2], f32x4 (&ra_fill)[4], const f32x4 (&ra_next)[4]) {
+  struct Frag {
+    f32x4 a[MT], b[JT];
+  };
+  auto read_frag = [&](Frag &f, int buf, int u) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      f.a[m] = *reinterpret_cast<const f32x4 *>(
+          &As[buf][(wm * MT * 32 + m * 32 + r) * kLdA + 8 * u + 4 * h]);
+#pragma unroll
+    for (int j = 0; j < JT; ++j) f.b[j] = Bs[buf][((wn * JT + j) * 4 + u) * 64 + lane];
+  };
+  auto mma = [&](const Frag &f) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < JT; ++j)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+          acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(f.a[m][q], f.b[j][q], acc[m][j], 0, 0, 0);
+  };
+  // stage s (reading buffer s & 1): stage s + 1's tiles (loaded two stages ago) go
+  // to the other buffer, stage s + 3's loads go out into the freed registers, then
+  // the stage's 4 groups with the next group's fragments read ahead (a group past
+  // the layer's K multiplies zero weights)
+  auto stage = [&](int s, f32x4 (&ra)[4], f32x4 (&rbv)[NTB]) {
     const int buf = s & 1;
-    f32x4 b[4][2];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[u][j] = bn[u][j];
-    if (s + 1 < nst) load_b(bn, s + 1);
-    if (s + 2 < nst) load_a(ra_fill, s + 2);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (s * 4 + u >= G) break;
-      f32x4 a[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-        a[m] = *reinterpret_cast<const f32x4 *>(
-            &As[buf][(wm * 64 + m * 32 + r) * kLdA + 8 * u + 4 * h]);
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int m = 0; m < 2; ++m)
-            acc[m][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m][q], b[u][j][q], acc[m][j], 0, 0, 0);
-    }
-    if (s + 1 < nst) store_a(ra_next, buf ^ 1);
+    store(ra, rbv, buf ^ 1);  // (past the last stage: zeros, never read)
+    load_b(rbv, s + 3);
+    load_a(ra, s + 3);
+    Frag f0, f1;
+    read_frag(f0, buf, 0);
+    read_frag(f1, buf, 1);
+    mma(f0);
+    read_frag(f0, buf, 2);
+    mma(f1);
+    read_frag(f1, buf, 3);
+    mma(f0);
+    mma(f1);
     __syncthreads();
   };
-  f32x4 bn[4][2];
-  load_b(bn, 0);
+  // prologue: stage 0 into buffer 0; stage 1's loads into set 1, stage 2's into set 0
+  f32x4 ra0[4], ra1[4], rb0[NTB], rb1[NTB];
+  load_b(rb0, 0);
   load_a(ra0, 0);
+  load_b(rb1, 1);
   load_a(ra1, 1);
-  store_a(ra0, 0);
+  store(ra0, rb0, 0);
+  load_b(rb0, 2);
+  load_a(ra0, 2);
   __syncthreads();
-  // even stages fill ra0 (stage s + 2) and store ra1 (stage s + 1); odd ones the reverse
-  for (int s = 0; s < nst; s += 2) {
-    stage(s, bn, ra0, ra1);
-    if (s + 1 < nst) stage(s + 1, bn, ra1, ra0);
+  // even stages store set 1 (stage s + 1) and refill it with stage s + 3; odd ones
+  // set 0.  Stages in pairs, both unconditional (an odd count gets a stage of zero
+  // weights): a conditional second stage left the loop head's wait for the first
+  // store at vmcnt(0) instead of vmcnt(8), one stage of load latency lost.
+  const int nst2 = (nst + 1) & ~1;
+  for (int s = 0; s < nst2; s += 2) {
+    stage(s, ra1, rb1);
+    stage(s + 1, ra0, rb0);
   }
   // bias (after the dot product, as Keras adds it) + activation, stored per
-  // accumulator element: lane (r, h) holds column r of rows (q&3) + 8(q>>2) + 4h
+  // accumulator element: lane (r, h) holds column r of rows (q&3) + 8(q>>2) + 4h;
+  // one store instruction writes two 128-byte row segments.  Stores through a
+  // descriptor over the panel's valid rows (past it they are dropped: no per-element
+  // branch), the activation chosen once per workgroup.
+  const auto rsC = __builtin_amdgcn_make_buffer_rsrc(
+      C + row0 * (int64_t)ldc, 0,
+      (int)((rows - row0 < kBM2 ? rows - row0 : kBM2) * (int64_t)ldc * 4), 0x00020000);
+  auto epilogue = [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int nt = nt0 + j;
-    if (nt >= NT) continue;
-    const int col = nt * 32 + r;
-    const float bv = bias[col];
+    for (int j = 0; j < JT; ++j) {
+      const int nt = ntb + wn * JT + j;
+      if (nt >= NT) continue;
+      const int col = nt * 32 + r;
+      const float bv = bias[col];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+      for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int64_t row = row0 + wm * 64 + m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-        if (row < rows) C[row * (int64_t)ldc + col] = act_apply(act, acc[m][j][q] + bv);
-      }
+        for (int q = 0; q < 16; ++q) {
+          const int row = wm * MT * 32 + m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
+          __builtin_amdgcn_raw_buffer_store_b32(
+              __builtin_bit_cast(uint32_t, act_apply(ACT, acc[m][j][q] + bv)), rsC,
+              (uint32_t)((row * ldc + col) * 4), 0, 0);
+        }
+    }
+  };
+  switch (act) {
+    case IK_ACT_TANH: epilogue(std::integral_constant<int, IK_ACT_TANH>{}); break;
+    case IK_ACT_RELU: epilogue(std::integral_constant<int, IK_ACT_RELU>{}); break;
+    case IK_ACT_SIGMOID: epilogue(std::integral_constant<int, IK_ACT_SIGMOID>{}); break;
+    default: epilogue(std::integral_constant<int, IK_ACT_LINEAR>{}); break;
   }
 }
 
@@ -252,6 +325,8 @@ int64_t ann_big_rows(const AnnBigModel &m, size_t act_bytes) {
   int64_t rows = (int64_t)(act_bytes / per_row) / annb::kBM * annb::kBM;
   return rows;
 }
+// (annb_gemm_kernel's buffer offsets are 32-bit: a panel's A is at most 128 rows of
+// 16384 floats, 8 MiB, and a block's weights 4 tiles x 2048 groups x 1 KiB, 8 MiB)
 
 void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, int64_t n,
                     float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
@@ -277,12 +352,21 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
     int cur = 0, lda = 8;
     for (const AnnBigLayer &L : m.layers) {
       const int G = L.kp / 8, NT = L.np / 32;
-      const int64_t nRB = (rows + kBM - 1) / kBM;
-      const dim3 grid((unsigned)((nRB + 7) / 8 * 8 * ((NT + 3) / 4)));
+      // whole groups of BH x BW tiles, a multiple of 8 groups (annb_gemm_kernel)
+      const int64_t nRB = (rows + kBM2 - 1) / kBM2;
+      const int ntb = NT == 1 ? 1 : 4;  // column tiles per workgroup
+      const int nCB = (NT + ntb - 1) / ntb, BW = nCB < 8 ? nCB : 8, BH = 64 / BW;
+      const int64_t groups = (nRB + BH - 1) / BH * ((nCB + BW - 1) / BW);
+      const dim3 grid((unsigned)((groups + 7) / 8 * 8 * BH * BW));
       kt_begin("annb_gemm_kernel", st);
-      hipLaunchKernelGGL(annb_gemm_kernel, grid, dim3(256), 0, st, buf[cur], lda, rows,
-                         reinterpret_cast<const f32x4 *>(L.wp), G, NT, L.bias, L.act,
-                         buf[cur ^ 1], L.np);
+      if (NT == 1)
+        hipLaunchKernelGGL(annb_gemm_kernel<1>, grid, dim3(256), 0, st, buf[cur], lda, rows,
+                           reinterpret_cast<const f32x4 *>(L.wp), G, NT, L.bias, L.act,
+                           buf[cur ^ 1], L.np);
+      else
+        hipLaunchKernelGGL(annb_gemm_kernel<2>, grid, dim3(256), 0, st, buf[cur], lda, rows,
+                           reinterpret_cast<const f32x4 *>(L.wp), G, NT, L.bias, L.act,
+                           buf[cur ^ 1], L.np);
       kt_end(st);
       cur ^= 1;
       lda = L.np;

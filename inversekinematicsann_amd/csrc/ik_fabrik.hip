@@ -748,6 +748,11 @@ fabrik_iter_kernel(FabArgs a) {
   double tol2 = a.tol2;
   int max_iter = a.max_iter;
   asm volatile("" : "+v"(tol2), "+v"(max_iter));
+  // the goal error's threshold as an opaque second copy: with one value on both
+  // compares, (se > t) || (ge > t) becomes max(se, ge) > t, three v_max_f64 (two
+  // canonicalizing) and a compare instead of two compares
+  double tol2g = tol2;
+  asm volatile("" : "+v"(tol2g));
   double L[4] = {a.r.links[0], a.r.links[1], a.r.links[2], a.r.links[3]};
 
   // prepared points: the batch's entry j in slot j of the wave's LDS batch
@@ -953,7 +958,7 @@ fabrik_iter_kernel(FabArgs a) {
     // iterate until a refill is due (REFILL_MIN lanes free) or, once the queue is
     // dry, until every lane has stopped: the refill's scalar state stays out of
     // this loop, so its SGPRs are not reloaded from their spill lanes per iteration
-    const int need = dry ? 64 : REFILL_MIN;
+    const int need = __builtin_amdgcn_readfirstlane(dry ? 64 : REFILL_MIN);  // (an SGPR)
     while (true) {
 #ifdef IKHIP_DIAG
     {
@@ -971,10 +976,10 @@ fabrik_iter_kernel(FabArgs a) {
     {
       // one divergent region per iteration: lanes that stop here become pending
       // (parked at the next refill) without a branch of their own
-      const bool run = active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step);
+      const bool run = active && st == IK_OK && ((se > tol2) || (ge > tol2g)) && (max_iter > step);
       pending = pending || (active && !run);
       active = run;
-      if (__popcll(__ballot(!run)) >= need) break;
+      if (__popcll(__builtin_amdgcn_ballot_w64(!run)) >= need) break;  // (a bool: no VGPR round trip)
       if (run) {
         if constexpr (CORE == 2) {
           uint32_t dom = 0, cdom_n = cdom;
