@@ -295,6 +295,8 @@ struct FabArgs {
   int64_t n;
   double tol;      // fabrik.py:57 err_margin, as given
   double tol2;     // tol_threshold(tol): the loop compares squared errors with it
+  ErrBand band;    // the lazy errors' band (fabrik_band) for lanes with |J0|_1 + |goal|_1 <= band_n1
+  double band_n1;
   int max_iter;
   int check_limits;
   double *ang;
@@ -784,12 +786,23 @@ fabrik_iter_kernel(FabArgs a) {
 
   bool active = false, pending = false;  // solving / finished but not yet parked
   int64_t out = 0;                       // the lane's point index
+  // J3: the effector; CORE 2 keeps it only from a fallback iteration (the fast
+  // step leaves it to the carry: effector() below)
   d3 J0 = {0, 0, 0}, J1 = J0, J2 = J0, J3 = J0, g = J0;
-  double se = 1.0, ge = 1.0;
+  bool cont = true;  // the reference's loop condition after the lane's last iteration
   int step = 0, st = IK_OK;
   double cq = 0.0;  // CORE == 2: the carried quotient, offset and domain value
   d3 cd = J0;
   uint32_t cdom = 0;
+  bool bok = false;  // CORE == 2: the launch's error band covers the lane (fabrik_step4_lazy)
+  // the effector F3 = get_point_between(F2, goal, L3): from the carry (cq, cd =
+  // goal - F2) whenever its radicand was in the core domain, else the fallback's J3
+  auto effector = [&]() -> d3 {
+    if constexpr (CORE == 2) {
+      if (cdom < kCoreDom) return {J2.x + (cq * cd.x), J2.y + (cq * cd.y), J2.z + (cq * cd.z)};
+    }
+    return J3;
+  };
 
 #ifdef IKHIP_DIAG
   // counters and stamps live in LDS (lane 0 writes), so that the diagnostic
@@ -836,14 +849,17 @@ fabrik_iter_kernel(FabArgs a) {
       if (np) {
         if (rcnt + np > 64) {
           IKHIP_DG(kDiagFlushes, 1);
+          IKHIP_DT_ACC(kDiagParkTicks, kDiagTSub);  // (the park's time excludes the flush)
           IKHIP_DT(kDiagTEnd);  // (scratch slot: the flush's start)
           ring_flush<ORD>(a, R, rcnt, lane, acc);
           prio_raise();  // (the flush dropped it)
           IKHIP_DT_ACC(kDiagFlushTicks, kDiagTEnd);
           IKHIP_DT_ACC(kDiagTRefill, kDiagTEnd);  // (not refill time)
+          IKHIP_DT(kDiagTSub);
           rcnt = 0;
         }
-        if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, g, out, step, st);
+        if (pending)
+          ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, effector(), g, out, step, st);
         pending = false;
         rcnt += np;
       }
@@ -942,11 +958,14 @@ fabrik_iter_kernel(FabArgs a) {
           g = {PB.v[9][src], PB.v[10][src], PB.v[11][src]};
           out = PB.idx[src];
           st = IK_OK;
-          se = 1.0;
-          ge = 1.0;
+          cont = true;  // the loop's initial errors of 1.0 (fabrik.py:53-54) exceed tol
           step = 0;
           active = true;
-          if constexpr (CORE == 2) reuse_carry(J2, g, L[3], cq, cd, cdom);
+          if constexpr (CORE == 2) {
+            reuse_carry(J2, g, L[3], cq, cd, cdom);
+            bok = fabs(J0.x) + fabs(J0.y) + fabs(J0.z) + fabs(g.x) + fabs(g.y) + fabs(g.z) <=
+                  a.band_n1;
+          }
         }
         pptr += take;
         handed += take;
@@ -963,7 +982,7 @@ fabrik_iter_kernel(FabArgs a) {
 #ifdef IKHIP_DIAG
     {
       const unsigned long long sm =
-          __ballot(active && st == IK_OK && ((se > tol2) || (ge > tol2)) && (max_iter > step));
+          __ballot(active && st == IK_OK && cont && (max_iter > step));
       IKHIP_DG(kDiagSteps, sm ? 1 : 0);
       IKHIP_DG(kDiagLaneSteps, __popcll(sm));
       if (dry) {  // the queue and the wave's batch are exhausted
@@ -976,27 +995,29 @@ fabrik_iter_kernel(FabArgs a) {
     {
       // one divergent region per iteration: lanes that stop here become pending
       // (parked at the next refill) without a branch of their own
-      const bool run = active && st == IK_OK && ((se > tol2) || (ge > tol2g)) && (max_iter > step);
+      const bool run = active && st == IK_OK && cont && (max_iter > step);
       pending = pending || (active && !run);
       active = run;
       if (__popcll(__builtin_amdgcn_ballot_w64(!run)) >= need) break;  // (a bool: no VGPR round trip)
       if (run) {
         if constexpr (CORE == 2) {
           uint32_t dom = 0, cdom_n = cdom;
-          d3 n1 = J1, n2 = J2, n3 = J3, cd_n = cd;
-          double se_n, ge_n, cq_n = cq;
-          fabrik_step4_reuse(J0, n1, n2, n3, g, L, se_n, ge_n, cq_n, cd_n, cdom_n, dom);
+          d3 n1 = J1, n2 = J2, cd_n = cd;
+          double cq_n = cq;
+          bool cont_n;
+          fabrik_step4_lazy(J0, n1, n2, g, L, a.band, bok, tol2, cont_n, cq_n, cd_n, cdom_n, dom);
           if (__all(dom < kCoreDom)) {
-            J1 = n1; J2 = n2; J3 = n3;
-            se = se_n;
-            ge = ge_n;
+            J1 = n1; J2 = n2;
             cq = cq_n;
             cd = cd_n;
             cdom = cdom_n;
+            cont = cont_n;
           } else {
             IKHIP_DG(kDiagFallbacks, 1);
+            double se, ge;
             fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
             reuse_carry(J2, g, L[3], cq, cd, cdom);
+            cont = (se > tol2) || (ge > tol2g);
           }
         } else if constexpr (CORE == 1) {
           // wave-uniform fallback: when any lane's radicand leaves sqrt_core's
@@ -1004,18 +1025,19 @@ fabrik_iter_kernel(FabArgs a) {
           // iteration with the general sqrt / division (and their errors)
           uint32_t dom = 0;
           d3 n1 = J1, n2 = J2, n3 = J3;
-          double se_n, ge_n;
-          fabrik_step4_core(J0, n1, n2, n3, g, L, se_n, ge_n, dom);
+          double se, ge;
+          fabrik_step4_core(J0, n1, n2, n3, g, L, se, ge, dom);
           if (__all(dom < kCoreDom)) {
             J1 = n1; J2 = n2; J3 = n3;
-            se = se_n;
-            ge = ge_n;
           } else {
             IKHIP_DG(kDiagFallbacks, 1);
             fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
           }
+          cont = (se > tol2) || (ge > tol2g);
         } else {
+          double se, ge;
           fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
+          cont = (se > tol2) || (ge > tol2g);
         }
         ++step;
       }
@@ -1033,7 +1055,8 @@ fabrik_iter_kernel(FabArgs a) {
       rcnt = 0;
     }
     IKHIP_DT(kDiagTDrain2);
-    if (pending) ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, J3, g, out, step, st);
+    if (pending)
+      ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, effector(), g, out, step, st);
     rcnt += np;
     IKHIP_DG(kDiagFlushes, 1);
     IKHIP_DT(kDiagTEnd);
@@ -1120,6 +1143,14 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   a.n = n;
   a.tol = tol;
   a.tol2 = tol_threshold(tol);
+  // the band covers goals well past the reach: 64 (1 + |d1| + |a1| + sum L)
+  {
+    const double sum_l = std::fabs(r.links[0]) + std::fabs(r.links[1]) + std::fabs(r.links[2]) +
+                         std::fabs(r.links[3]);
+    a.band_n1 = 64.0 * (1.0 + std::fabs(r.dh[4]) + std::fabs(r.dh[8]) + sum_l);
+    if (!std::isfinite(a.band_n1)) a.band_n1 = -1.0;  // (no lane: every comparison exact)
+    a.band = fabrik_band(a.tol2, a.band_n1, sum_l);
+  }
   a.max_iter = max_iter;
   a.check_limits = check_limits ? 1 : 0;
   a.ang = ang;

@@ -95,3 +95,98 @@ __device__ __forceinline__ void reuse_carry(const d3 c2, const d3 g, double L3, 
 }
 
 }  // namespace ikhip
+
+namespace ikhip {
+
+// ---- the loop condition without the start and goal errors' own arithmetic ----
+// fabrik.py:57-64 continues while se > tol or ge > tol, se = |B0 - start| and
+// ge = |F3 - goal| (squared here, against tol2).  With q = L0 / |b1 - start| the
+// start error is |(q - 1) (start - b1)| up to roundings, and with the carried
+// quotient cq the goal error is |(cq - 1) (goal - c2)|: se2a = (1 - q)^2 x and
+// ge2a = (1 - cq)^2 x3 from the radicands the step computes anyway.  The
+// reference's own se2 / ge2 (b0, F3 = c3 and their differences, 25 VALU) are
+// computed only when an approximation falls inside the lane's band [lo, hi]
+// (ErrBand): outside it the comparison with tol2 provably comes out the same.
+//
+// The band (band_for): with u = 2^-53, every rounding of b0 = b1 + q (start - b1),
+// B0 - start and of the squares moves |B0 - start| by at most
+//   D <= 1.03 u (3 |goal| + 2 |start| + 3 sum L)
+// (the backward points lie within sum L of the goal, the forward ones within sum L
+// of the start; the same bound with the roles swapped covers the goal error), and
+// the relative errors of se2a and se2 are below 8u and 3u.  With T = sqrt(tol2):
+//   se2a > hi = (D + T)^2 (1 + 2^-36)        =>  se2 > tol2
+//   se2a < lo = (T - D)^2 (1 - 2^-36)        =>  se2 <= tol2   (only if D <= T / 2)
+// The band is one per launch (fabrik_band on the host): D from a bound n1max on
+// |start|_1 + |goal|_1, D = 2u (3 n1max + 4 sum L + 1) (twice the bound; L1 norms
+// bound the Euclidean ones), with T's bounds tol_lo <= T <= tol_hi.  A lane past
+// n1max (or with a non-finite goal) carries bok = false: its comparisons are exact.
+struct ErrBand {
+  double lo, hi;
+};
+
+__host__ __forceinline__ ErrBand fabrik_band(double tol2, double n1max, double sum_l) {
+  ErrBand b = {-1.0, 0.0};
+  if (!(tol2 > 0.0)) return b;  // (hi = 0, lo = -1: every positive error exact)
+  const double T = std::sqrt(tol2);
+  const double tol_lo = T * (1.0 - 0x1p-50), tol_hi = T * (1.0 + 0x1p-50);
+  const double d = 0x1p-52 * (3.0 * n1max + 4.0 * sum_l + 1.0);
+  const double h = d + tol_hi;
+  b.hi = (h * h) * (1.0 + 0x1p-36);
+  const double l = tol_lo - d;
+  b.lo = (d <= 0.5 * tol_lo) ? (l * l) * (1.0 - 0x1p-36) : -1.0;
+  return b;
+}
+
+// fabrik_step4_reuse with the loop condition cont = (se2 > tol2) || (ge2 > tol2)
+// decided through the band, and F3 (c3 = c2 + cq cd, the reference's
+// get_point_between(c2, goal, L3) from the carry) left to the caller.  The exact
+// se2 / ge2 run in a wave-uniform branch when any lane's approximation is uncertain
+// (and for the goal error only where the start error has not already decided).
+__device__ __forceinline__ void fabrik_step4_lazy(const d3 start, d3 &c1, d3 &c2, const d3 g,
+                                                  const double *L, const ErrBand band,
+                                                  bool bok, double tol2, bool &cont, double &cq, d3 &cd,
+                                                  uint32_t &cdom, uint32_t &dom) {
+  dom = cdom;
+  const d3 b2 = {g.x - cq * cd.x, g.y - cq * cd.y, g.z - cq * cd.z};
+  const d3 b1 = point_between_core(b2, c1, L[1], dom);
+  const double dx = start.x - b1.x, dy = start.y - b1.y, dz = start.z - b1.z;
+  const double x = sq(dx) + sq(dy) + sq(dz);
+  dom = max(dom, sqrt_core_dom(x));
+  const double q = div_core(L[0], sqrt_core(x));
+  const double qx = q * dx, qy = q * dy, qz = q * dz;
+  // the decisions as lane masks (ballots of the compares): the band tests, the
+  // merges with the exact results and the uncertainty are scalar-ALU operations
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  const uint64_t nbok = __builtin_amdgcn_ballot_w64(!bok);
+  const double t = 1.0 - q;
+  const double se2a = (t * t) * x;
+  uint64_t gt = __builtin_amdgcn_ballot_w64(se2a > band.hi);
+  uint64_t unc = (ex & ~(gt | __builtin_amdgcn_ballot_w64(se2a < band.lo))) | nbok;
+  if (__builtin_expect(unc != 0, 0)) {  // (a NaN is uncertain)
+    const d3 b0 = {b1.x + qx, b1.y + qy, b1.z + qz};
+    const double se2 = dist3_sq(b0, start);
+    gt = (gt & ~unc) | (__builtin_amdgcn_ballot_w64(se2 > tol2) & unc);
+  }
+  c1 = {start.x - qx, start.y - qy, start.z - qz};
+  c2 = point_between_core(c1, b2, L[2], dom);
+  const double ex3 = g.x - c2.x, ey3 = g.y - c2.y, ez3 = g.z - c2.z;
+  const double x3 = sq(ex3) + sq(ey3) + sq(ez3);
+  cdom = sqrt_core_dom(x3);
+  dom = max(dom, cdom);
+  cq = div_core(L[3], sqrt_core(x3));
+  cd = {ex3, ey3, ez3};
+  const double t3 = 1.0 - cq;
+  const double ge2a = (t3 * t3) * x3;
+  uint64_t gt3 = __builtin_amdgcn_ballot_w64(ge2a > band.hi);
+  // (the goal error only matters where the start error has not decided already)
+  uint64_t unc3 =
+      ((ex & ~(gt3 | __builtin_amdgcn_ballot_w64(ge2a < band.lo))) | nbok) & ~gt;
+  if (__builtin_expect(unc3 != 0, 0)) {
+    const d3 c3 = {c2.x + (cq * ex3), c2.y + (cq * ey3), c2.z + (cq * ez3)};
+    const double ge2 = dist3_sq(c3, g);
+    gt3 = (gt3 & ~unc3) | (__builtin_amdgcn_ballot_w64(ge2 > tol2) & unc3);
+  }
+  cont = __builtin_amdgcn_inverse_ballot_w64(gt | gt3);
+}
+
+}  // namespace ikhip
