@@ -643,25 +643,37 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
 // angles step on it, one entry per lane (finish_point).  So the seed pose and
 // the joints never travel through HBM, and neither step runs at the width of
 // the handful of lanes that finish together.
+// A parked point is one 144-byte record per slot, written and read as nine
+// 16-byte words (ds_write_b128 / ds_read_b128): the joints, the goal (for the FK
+// round trip, not read from HBM again) and {index, iterations, status}.  The
+// 36-dword slot stride puts 16 lanes' words on 64 distinct banks.
 struct RetireRing {
-  double j[12][64];
-  double g[3][64];  // the goal, for the FK round trip (not read from HBM again)
-  long long idx[64];
-  int it[64];
-  int st[64];
+  double2 w[64][9];
 };
 
 __device__ __forceinline__ void ring_put(RetireRing &R, int s, const d3 &J0, const d3 &J1,
                                          const d3 &J2, const d3 &J3, const d3 &g, int64_t idx,
                                          int it, int st) {
-  R.j[0][s] = J0.x; R.j[1][s] = J0.y; R.j[2][s] = J0.z;
-  R.j[3][s] = J1.x; R.j[4][s] = J1.y; R.j[5][s] = J1.z;
-  R.j[6][s] = J2.x; R.j[7][s] = J2.y; R.j[8][s] = J2.z;
-  R.j[9][s] = J3.x; R.j[10][s] = J3.y; R.j[11][s] = J3.z;
-  R.g[0][s] = g.x; R.g[1][s] = g.y; R.g[2][s] = g.z;
-  R.idx[s] = idx;
-  R.it[s] = it;
-  R.st[s] = st;
+  double2 *w = R.w[s];
+  w[0] = {J0.x, J0.y};
+  w[1] = {J0.z, J1.x};
+  w[2] = {J1.y, J1.z};
+  w[3] = {J2.x, J2.y};
+  w[4] = {J2.z, J3.x};
+  w[5] = {J3.y, J3.z};
+  w[6] = {g.x, g.y};
+  w[7] = {g.z, 0.0};
+  w[8] = {__longlong_as_double(idx),
+          __longlong_as_double((long long)(((uint64_t)(uint32_t)st << 32) | (uint32_t)it))};
+}
+
+__device__ __forceinline__ void ring_joints(const RetireRing &R, int s, d3 *J) {
+  const double2 *w = R.w[s];
+  const double2 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5];
+  J[0] = {w0.x, w0.y, w1.x};
+  J[1] = {w1.y, w2.x, w2.y};
+  J[2] = {w3.x, w3.y, w4.x};
+  J[3] = {w4.y, w5.x, w5.y};
 }
 
 // The angles step over the ring's first cnt entries (the whole wave calls it).
@@ -694,19 +706,20 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
   // barrier keeps the compiler from holding them in registers across the step)
   auto joints = [&](d3 *J) {
     asm volatile("" ::: "memory");
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      J[k] = {R.j[3 * k][lane], R.j[3 * k + 1][lane], R.j[3 * k + 2][lane]};
+    ring_joints(R, lane, J);
   };
-  int st = has ? R.st[lane] : IK_OK;
+  const double2 meta = R.w[lane][8];
+  const uint64_t itst = (uint64_t)__double_as_longlong(meta.y);
+  int st = has ? (int)(itst >> 32) : IK_OK;
   double th[4];
   angles_step(has, joints, st, th);
   if (has) {
     d3 J[4];
     joints(J);
-    const int64_t i = R.idx[lane];
-    const int it = R.it[lane];
-    commit_point(a, i, J, {R.g[0][lane], R.g[1][lane], R.g[2][lane]}, it, st, th, acc);
+    const int64_t i = __double_as_longlong(meta.x);
+    const int it = (int)(uint32_t)itst;
+    const double2 g01 = R.w[lane][6], g2 = R.w[lane][7];
+    commit_point(a, i, J, {g01.x, g01.y, g2.x}, it, st, th, acc);
     if constexpr (ORD) {
       if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample) {
         const uint32_t lo = (uint32_t)(it < 0xffff ? it : 0xffff);
@@ -759,9 +772,8 @@ fabrik_iter_kernel(FabArgs a) {
 
   // prepared points: the batch's entry j in slot j of the wave's LDS batch
   // (wave-uniform count / cursor); a refilled lane reads its entry from there
-  struct PrepBatch {
-    double v[12][64];  // seed joints 0..2 and the goal
-    long long idx[64];
+  struct PrepBatch {  // per entry seven 16-byte words: seed joints 0..2, goal, index
+    double2 w[64][7];
   };
   __shared__ PrepBatch batches[4];
   PrepBatch &PB = batches[threadIdx.x >> 6];
@@ -934,11 +946,14 @@ fabrik_iter_kernel(FabArgs a) {
               atomicMin(&a.S->first_oob, (unsigned long long)ni);
             d3 Js[4];
             (void)seed_pose((const RobotConstDev *)k, ng, Js);
-            PB.v[0][lane] = Js[0].x; PB.v[1][lane] = Js[0].y; PB.v[2][lane] = Js[0].z;
-            PB.v[3][lane] = Js[1].x; PB.v[4][lane] = Js[1].y; PB.v[5][lane] = Js[1].z;
-            PB.v[6][lane] = Js[2].x; PB.v[7][lane] = Js[2].y; PB.v[8][lane] = Js[2].z;
-            PB.v[9][lane] = ng.x; PB.v[10][lane] = ng.y; PB.v[11][lane] = ng.z;
-            PB.idx[lane] = ni;
+            double2 *w = PB.w[lane];
+            w[0] = {Js[0].x, Js[0].y};
+            w[1] = {Js[0].z, Js[1].x};
+            w[2] = {Js[1].y, Js[1].z};
+            w[3] = {Js[2].x, Js[2].y};
+            w[4] = {Js[2].z, ng.x};
+            w[5] = {ng.y, ng.z};
+            w[6] = {__longlong_as_double(ni), 0.0};
           }
 #ifdef IKHIP_DIAG
           // (the seed's loads are consumed before the stamp)
@@ -952,11 +967,13 @@ fabrik_iter_kernel(FabArgs a) {
         const int src = mine ? pptr + (rank - handed) : lane;
         __builtin_amdgcn_wave_barrier();  // the batch's LDS writes before the reads
         if (mine) {
-          J0 = {PB.v[0][src], PB.v[1][src], PB.v[2][src]};
-          J1 = {PB.v[3][src], PB.v[4][src], PB.v[5][src]};
-          J2 = {PB.v[6][src], PB.v[7][src], PB.v[8][src]};
-          g = {PB.v[9][src], PB.v[10][src], PB.v[11][src]};
-          out = PB.idx[src];
+          const double2 *w = PB.w[src];
+          const double2 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5];
+          J0 = {w0.x, w0.y, w1.x};
+          J1 = {w1.y, w2.x, w2.y};
+          J2 = {w3.x, w3.y, w4.x};
+          g = {w4.y, w5.x, w5.y};
+          out = __double_as_longlong(w[6].x);
           st = IK_OK;
           cont = true;  // the loop's initial errors of 1.0 (fabrik.py:53-54) exceed tol
           step = 0;
