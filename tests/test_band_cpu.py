@@ -1,0 +1,108 @@
+"""The FABRIK loop condition's error band (csrc/ik_fabrik_step.h, fabrik_step4_lazy /
+fabrik_band), checked numerically on the CPU: along real FABRIK iterations (numpy
+float64, the reference's arithmetic: kinematics/point.py:25-45, fabrik.py:19-64),
+the start and goal errors the step approximates from its radicands,
+(1 - q)^2 x and (1 - cq)^2 x3, stay within the band's D of the reference's own
+|B0 - start| and |F3 - goal|, and the band's decisions agree with the exact
+comparison for thresholds placed right at the errors.  The GPU tests check the
+kernel bit for bit; this pins the bound the kernel's proof rests on, including the
+converged states where the errors are tiny and the approximation is all roundoff.
+"""
+import numpy as np
+
+U = 2.0 ** -53
+
+
+def pb(s, e, d):
+    """get_point_between(s, e, d) and its radicand / quotient, batched."""
+    dv = e - s
+    x = (dv[:, 0] * dv[:, 0] + dv[:, 1] * dv[:, 1]) + dv[:, 2] * dv[:, 2]
+    q = d / np.sqrt(x)
+    return s + q[:, None] * dv, x, q
+
+
+def band(tol2, n1max, sum_l):
+    """fabrik_band (ik_fabrik_step.h), restated."""
+    T = np.sqrt(tol2)
+    tlo, thi = T * (1.0 - 2.0 ** -50), T * (1.0 + 2.0 ** -50)
+    d = 2.0 ** -52 * (3.0 * n1max + 4.0 * sum_l + 1.0)
+    hi = ((d + thi) ** 2) * (1.0 + 2.0 ** -36)
+    lo = ((tlo - d) ** 2) * (1.0 - 2.0 ** -36) if d <= 0.5 * tlo else -1.0
+    return lo, hi, d
+
+
+def chains(n, rng):
+    start = np.tile([0.0, 0.0, 2.0], (n, 1))
+    J = [start]
+    for _ in range(3):
+        u = rng.normal(size=(n, 3))
+        u /= np.linalg.norm(u, axis=1, keepdims=True)
+        J.append(J[-1] + 2.0 * u)
+    g = start + rng.uniform(-7.5, 7.5, size=(n, 3))
+    return J, g
+
+
+def test_band_bounds_the_approximate_errors():
+    rng = np.random.default_rng(5)
+    L = 2.0
+    n = 20000
+    J, g = chains(n, rng)
+    start, c1, c2 = J[0], J[1], J[2]
+    n1 = np.abs(start).sum(1) + np.abs(g).sum(1)
+    worst = 0.0
+    for it in range(80):
+        b2, _, _ = pb(g, c2, L)
+        b1, _, _ = pb(b2, c1, L)
+        b0, x, q = pb(b1, start, L)
+        se = np.sqrt(((b0 - start) ** 2).sum(1))
+        sea = np.abs(1.0 - q) * np.sqrt(x)
+        c1, _, _ = pb(start, b1, L)
+        c2, _, _ = pb(c1, b2, L)
+        c3, x3, cq = pb(c2, g, L)
+        ge = np.sqrt(((c3 - g) ** 2).sum(1))
+        gea = np.abs(1.0 - cq) * np.sqrt(x3)
+        d = 2.0 ** -52 * (3.0 * n1 + 4.0 * 4 * L + 1.0)
+        ok = np.isfinite(se) & np.isfinite(ge)
+        # the kernel's D is twice the bound it needs; the observed gap stays below half
+        r = np.maximum(np.abs(se - sea), np.abs(ge - gea))[ok] / d[ok]
+        worst = max(worst, float(r.max()))
+        assert (r <= 0.5).all(), (it, float(r.max()))
+    assert worst > 0.0  # the comparison did see roundoff
+
+
+def test_band_decisions_match_exact_comparisons():
+    """Thresholds from 1e-6 relative down to one ulp around the errors themselves:
+    wherever the band decides, it decides as the exact squared comparison does (and
+    the thresholds closest to the error are left to the exact comparison)."""
+    rng = np.random.default_rng(6)
+    L = 2.0
+    J, g = chains(4000, rng)
+    start, c1, c2 = J[0], J[1], J[2]
+    n1max = float((np.abs(start).sum(1) + np.abs(g).sum(1)).max())
+    checked = undecided = 0
+    rel = [1e-6, 1e-9, 1e-11, 1e-12, 1e-13, 1e-14]
+    facs = [1.0 - r for r in rel] + [1.0 + r for r in rel]
+    for it in range(40):
+        b2, _, _ = pb(g, c2, L)
+        b1, _, _ = pb(b2, c1, L)
+        b0, x, q = pb(b1, start, L)
+        se2 = ((b0 - start) ** 2).sum(1)
+        se2a = ((1.0 - q) * (1.0 - q)) * x
+        c1, _, _ = pb(start, b1, L)
+        c2, _, _ = pb(c1, b2, L)
+        for k in range(0, len(se2), 97):
+            ts = [se2[k] * f for f in facs] + [se2[k], np.nextafter(se2[k], 0),
+                                               np.nextafter(se2[k], 1), se2a[k]]
+            for tol2 in ts:
+                if not (tol2 > 0 and np.isfinite(tol2)):
+                    continue
+                lo, hi, _ = band(tol2, n1max, 4 * L)
+                if se2a[k] > hi:
+                    assert se2[k] > tol2
+                    checked += 1
+                elif se2a[k] < lo:
+                    assert se2[k] <= tol2
+                    checked += 1
+                else:
+                    undecided += 1
+    assert checked > 5000 and undecided > 1000
