@@ -51,6 +51,8 @@ for tol, mi in ((1e-3, 100), (1e-5, 200)):
     c["prep_us_per_wave"] = c["prep_ticks"] / 100.0 / max(c["waves"], 1)
     for k in ("refill", "park", "stage"):
         c[k + "_us_per_wave"] = c[k + "_ticks"] / 100.0 / max(c["waves"], 1)
+    # the refill's rest: handing prepared entries to the free lanes
+    c["handout_us_per_wave"] = c["refill_us_per_wave"] - c["park_us_per_wave"] - c["stage_us_per_wave"]
     c["pct"] = pc
     c["wave_start_us"] = us(t[:, T0])
     c["wave_dry_us"] = us(t[:, TDRY])       # queue and the wave's batch exhausted
