@@ -48,7 +48,8 @@ FP16_MFMA_PEAK = 2.5e15     # dense fp16 matrix peak (no sparsity)
 SPLIT_PRODUCTS = {"bf16x6": 6, "fp16x3": 3}  # MFMA products per fp32 product
 FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
 HBM_PEAK = 8.0e12           # bytes/s
-FABRIK_FLOP_PER_ITER = 132
+FABRIK_FLOP_PER_ITER = 132  # per executed reference iteration
+FABRIK_FLOP_PER_POINT = 150  # + the seed FK and angles, per point
 
 
 def launch_command(argv, gpus, port):
@@ -586,8 +587,11 @@ def run_fabrik(job, args, tol=None, max_iter=None):
             job, lambda hp, pinned: _host_fabrik(job, hp, pinned, tol, max_iter), args)
     # this rank's own iterations (the kernel's work), from its shard of the rows
     local_iters = sum(int(dit[b:e].sum().item()) for b, e in _own_parts(job))
+    local_points = sum(e - b for b, e in _own_parts(job))
     k = res["kernels"].get("fabrik_iter_kernel")
-    flops = FABRIK_FLOP_PER_ITER * local_iters
+    # 132 flop per iteration + 150 per point (seed and angles, both in
+    # this kernel)
+    flops = FABRIK_FLOP_PER_ITER * local_iters + FABRIK_FLOP_PER_POINT * local_points
     pkey = "fabrik_iter_kernel" if (tol, max_iter) != (1e-5, 200) else \
         "fabrik_tol1e-5/fabrik_iter_kernel"
     traffic = load_traffic(args.traffic_file, pkey)
@@ -601,7 +605,9 @@ def run_fabrik(job, args, tol=None, max_iter=None):
                        "frac_headline": fr["headline"],
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
+                       "algorithmic_flop_per_point": FABRIK_FLOP_PER_POINT,
                        "iterations_per_launch": local_iters,
+                       "points_per_launch": local_points,
                        **prof,
                        # the flop count prices a correctly rounded sqrt / division as
                        # one flop; the pipes say how busy the SIMDs actually are
