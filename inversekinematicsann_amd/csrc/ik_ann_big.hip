@@ -9,9 +9,11 @@
 //   annb_in_kernel     workspace check + StandardScaler.transform (float64) -> fp32
 //                      rows of 8 (x, y, z, 0...)
 //   annb_gemm_kernel   Y = act(X @ W + b), exact-fp32 v_mfma_f32_32x32x2_f32;
-//                      256 x 128 output tiles, 8 waves each 64 x 64, the X tile and
+//                      128 x 128 output tiles, 4 waves each 64 x 64, the X tile and
 //                      the weights (the fused kernel's packed fragment order,
 //                      ann_pack_layer) double-buffered through LDS 32 deep in K
+//   annb_gemm_x6_kernel  the same layer in the bf16x6 mode (IK_ANN_BF16X6): six
+//                      bf16 products per fp32 one on v_mfma_f32_16x16x32_bf16
 //   annb_out_kernel    StandardScaler.inverse_transform (in-place fp32, float64
 //                      ops) + the cli.py:54-61 FK round trip + stats, as the fused
 //                      kernel's epilogue does
@@ -20,6 +22,7 @@
 // activation budget.  Still one library call (ik_ann_solve): the chunk loop is
 // host code on the context's stream.
 #include <cmath>
+#include <cstring>
 #include <type_traits>
 
 #include "ik_common.h"
@@ -29,6 +32,10 @@ namespace annb {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBM = 128;      // chunk granularity of the activation buffers (rows)
 constexpr int kBK = 32;       // K per LDS stage (4 groups of 8)
@@ -274,6 +281,186 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_kernel(const float *__restri
   }
 }
 
+// ---------------------------------------------------------------- bf16x6 ----
+// The layer in the split mode (IK_ANN_BF16X6, as the fused kernel's, ik_ann.hip
+// "split-bf16"): x = hi + mid + lo in bf16 (each residual exact in fp32) for both
+// operands, and the six products above 2^-24 -- W.hi X.lo, W.mid X.mid, W.lo X.hi,
+// W.hi X.mid, W.mid X.hi, W.hi X.hi, smallest first -- accumulated in fp32 by
+// v_mfma_f32_16x16x32_bf16 (exact bf16 products): fp32-level results at 6 bf16
+// MFMAs (96 cycles) per 16 x 16 x 32 block instead of 16 fp32 ones (256).
+//
+// Tile 128 points x 128 features, 4 waves of 64 x 64 (4 x 4 accumulators of 16 x
+// 16), two workgroups per CU.  The weights are the MFMA's A operand (16 features
+// x 32 k) and the activations its B operand (32 k x 16 points), so a lane's
+// accumulator holds 4 consecutive features of one point: one 16-byte store.
+// Stages of 32 in K through LDS (one buffer each for the activations' and the
+// weights' three planes, 60 KiB): the activations arrive fp32 from HBM and are
+// split as they are written to LDS, the weights arrive split (ann_big_pack_x:
+// [plane][K / 32][features][32] bf16).  The next stage's loads are issued
+// before the current stage's MFMAs, into registers.
+constexpr int kXLd = 40;  // LDS row stride in bf16 (80 B: 16 lanes' rows on distinct banks)
+
+struct Split3 {
+  bf16x8 hi, mid, lo;
+};
+
+__device__ __forceinline__ Split3 split3(f32x4 a, f32x4 b) {
+  const float x[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  u32x4 h, m, l;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 v = {x[2 * i], x[2 * i + 1]};
+    const uint32_t ph = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+    const f32x2 vh = {__builtin_bit_cast(float, ph << 16),
+                      __builtin_bit_cast(float, ph & 0xffff0000u)};
+    const f32x2 r1 = v - vh;
+    const uint32_t pm = __builtin_bit_cast(uint32_t, __builtin_convertvector(r1, bf16x2));
+    const f32x2 vm = {__builtin_bit_cast(float, pm << 16),
+                      __builtin_bit_cast(float, pm & 0xffff0000u)};
+    const f32x2 r2 = r1 - vm;
+    h[i] = ph;
+    m[i] = pm;
+    l[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(r2, bf16x2));
+  }
+  return {__builtin_bit_cast(bf16x8, h), __builtin_bit_cast(bf16x8, m),
+          __builtin_bit_cast(bf16x8, l)};
+}
+
+__global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
+    const float *__restrict__ A, int lda, int64_t rows, const uint16_t *__restrict__ wx, int KG,
+    int NP, const float *__restrict__ bias, int act, float *__restrict__ C, int ldc) {
+  __shared__ __attribute__((aligned(16))) uint16_t Xs[3][kBM2 * kXLd];  // 3 x 10 KiB
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[3][kBM2 * kXLd];  // 3 x 10 KiB
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves of 64 points x 64 features
+  // the fp32 kernel's XCD-aware 2-D tile groups (128 features = 4 column tiles)
+  const int NT = NP / 32;
+  const int nCB = (NT + 3) / 4;
+  const int64_t nRB = (rows + kBM2 - 1) / kBM2;
+  const int BW = nCB < 8 ? nCB : 8, BH = 64 / BW, per = BH * BW;
+  const int nBC = (nCB + BW - 1) / BW;
+  const unsigned b = blockIdx.x, xcd = b & 7u, kx = b >> 3;
+  const int64_t grp = (int64_t)(kx / (unsigned)per) * 8 + xcd;
+  const int inb = (int)(kx % (unsigned)per);
+  const int64_t rb = (grp / nBC) * BH + inb / BW;
+  const int cb = (int)(grp % nBC) * BW + inb % BW;
+  if (rb >= nRB || cb >= nCB) return;  // the grid is padded to whole groups
+  const int64_t row0 = rb * kBM2;
+  const int n0 = cb * 128;  // the block's first feature
+  f32x4 acc[4][4];          // [point subtile][feature subtile]
+#pragma unroll
+  for (int pm = 0; pm < 4; ++pm)
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) acc[pm][fm] = (f32x4)(0.0f);
+
+  const uint32_t kOOB = 0x80000000u;
+  const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float *>(A) + row0 * (int64_t)lda, 0,
+      (int)((rows - row0 < kBM2 ? rows - row0 : kBM2) * (int64_t)lda * 4), 0x00020000);
+  const auto rsW = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint16_t *>(wx), 0, (int)((size_t)3 * KG * NP * 64), 0x00020000);
+  // stage s: activations, 8 k of point (b >> 2) at k block (b & 3) for b = tid,
+  // tid + 256 (two 16-byte loads each); weights, plane i >> 1, 16 bytes of feature
+  // row (c >> 2) at k block (c & 3) for c = 256 (i & 1) + tid
+  auto load = [&](f32x4 (&ra)[4], u32x4 (&rw)[6], int s) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int bb = tid + 256 * i, p = bb >> 2, kb = bb & 3;
+      const uint32_t off = s < KG ? (uint32_t)((p * lda + s * 32 + 8 * kb) * 4) : kOOB;
+      ra[2 * i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
+      ra[2 * i + 1] =
+          __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off + 16, 0, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int c = 256 * (i & 1) + tid, n = c >> 2, kb = c & 3, pl = i >> 1;
+      const uint32_t off = (s < KG && n0 + n < NP)
+                               ? (uint32_t)(((((size_t)pl * KG + s) * NP + n0 + n) * 32 + 8 * kb) * 2)
+                               : kOOB;
+      rw[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsW, off, 0, 0));
+    }
+  };
+  auto store = [&](const f32x4 (&ra)[4], const u32x4 (&rw)[6]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int bb = tid + 256 * i, p = bb >> 2, kb = bb & 3;
+      const Split3 x = split3(ra[2 * i], ra[2 * i + 1]);
+      *reinterpret_cast<bf16x8 *>(&Xs[0][p * kXLd + 8 * kb]) = x.hi;
+      *reinterpret_cast<bf16x8 *>(&Xs[1][p * kXLd + 8 * kb]) = x.mid;
+      *reinterpret_cast<bf16x8 *>(&Xs[2][p * kXLd + 8 * kb]) = x.lo;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int c = 256 * (i & 1) + tid, n = c >> 2, kb = c & 3, pl = i >> 1;
+      *reinterpret_cast<u32x4 *>(&Ws[pl][n * kXLd + 8 * kb]) = rw[i];
+    }
+  };
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  f32x4 ra[4];
+  u32x4 rw[6];
+  load(ra, rw, 0);
+  for (int s = 0; s < KG; ++s) {
+    __syncthreads();  // the last stage's fragments are read
+    store(ra, rw);
+    __syncthreads();
+    load(ra, rw, s + 1);  // (past the last stage: out of range, zeros, never stored)
+    bf16x8 xf[4][3];
+#pragma unroll
+    for (int pm = 0; pm < 4; ++pm)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        xf[pm][pl] = *reinterpret_cast<const bf16x8 *>(
+            &Xs[pl][(wm * 64 + pm * 16 + fr) * kXLd + fk]);
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) {
+      bf16x8 wf[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        wf[pl] = *reinterpret_cast<const bf16x8 *>(&Ws[pl][(wn * 64 + fm * 16 + fr) * kXLd + fk]);
+#pragma unroll
+      for (int pm = 0; pm < 4; ++pm) {
+        f32x4 c = acc[pm][fm];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], xf[pm][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], xf[pm][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[2], xf[pm][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], xf[pm][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], xf[pm][0], c, 0, 0, 0);
+        acc[pm][fm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], xf[pm][0], c, 0, 0, 0);
+      }
+    }
+  }
+  // bias + activation: lane (fr, lane >> 4) of accumulator (pm, fm) holds features
+  // 4 (lane >> 4) .. + 3 of feature subtile fm for point fr of point subtile pm
+  const auto rsC = __builtin_amdgcn_make_buffer_rsrc(
+      C + row0 * (int64_t)ldc, 0,
+      (int)((rows - row0 < kBM2 ? rows - row0 : kBM2) * (int64_t)ldc * 4), 0x00020000);
+  auto epilogue = [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) {
+      const int f = n0 + wn * 64 + fm * 16;  // (NP is a multiple of 32: whole subtiles)
+      if (f >= NP) continue;
+      const int col = f + 4 * (lane >> 4);
+      const f32x4 bv = *reinterpret_cast<const f32x4 *>(bias + col);
+#pragma unroll
+      for (int pm = 0; pm < 4; ++pm) {
+        const int p = wm * 64 + pm * 16 + fr;
+        f32x4 v;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = act_apply(ACT, acc[pm][fm][i] + bv[i]);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rsC,
+                                               (uint32_t)((p * ldc + col) * 4), 0, 0);
+      }
+    }
+  };
+  switch (act) {
+    case IK_ACT_TANH: epilogue(std::integral_constant<int, IK_ACT_TANH>{}); break;
+    case IK_ACT_RELU: epilogue(std::integral_constant<int, IK_ACT_RELU>{}); break;
+    case IK_ACT_SIGMOID: epilogue(std::integral_constant<int, IK_ACT_SIGMOID>{}); break;
+    default: epilogue(std::integral_constant<int, IK_ACT_LINEAR>{}); break;
+  }
+}
+
 // Output: StandardScaler.inverse_transform (in-place fp32 with float64 operands,
 // as the fused kernel's epilogue) + the FK round trip and its batch stats.
 struct OutArgs {
@@ -328,9 +515,44 @@ int64_t ann_big_rows(const AnnBigModel &m, size_t act_bytes) {
 // (annb_gemm_kernel's buffer offsets are 32-bit: a panel's A is at most 128 rows of
 // 16384 floats, 8 MiB, and a block's weights 4 tiles x 2048 groups x 1 KiB, 8 MiB)
 
+// (host) round to nearest even, as v_cvt_pk_bf16_f32 does on the device
+static uint16_t bf16_rne_h(float x) {
+  uint32_t u;
+  std::memcpy(&u, &x, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)(u >> 16);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static float bf16_f32_h(uint16_t h) {
+  const uint32_t u = (uint32_t)h << 16;
+  float x;
+  std::memcpy(&x, &u, 4);
+  return x;
+}
+
+void ann_big_pack_x(const float *W, int k, int n, void *dst) {
+  const int KG = (k + 31) / 32, NP = (n + 31) / 32 * 32;
+  uint16_t *d = static_cast<uint16_t *>(dst);
+  const size_t plane = (size_t)KG * NP * 32;
+  for (int g = 0; g < KG; ++g)
+    for (int c = 0; c < NP; ++c)
+      for (int kk = 0; kk < 32; ++kk) {
+        const int kr = 32 * g + kk;
+        const float x = (kr < k && c < n) ? W[(size_t)kr * n + c] : 0.0f;
+        const uint16_t h = bf16_rne_h(x);
+        const float r1 = x - bf16_f32_h(h);
+        const uint16_t m = bf16_rne_h(r1);
+        const float r2 = r1 - bf16_f32_h(m);
+        const size_t at = ((size_t)g * NP + c) * 32 + kk;
+        d[at] = h;
+        d[plane + at] = m;
+        d[2 * plane + at] = bf16_rne_h(r2);
+      }
+}
+
 void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, int64_t n,
                     float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
-                    float *act, int64_t chunk_rows) {
+                    float *act, int64_t chunk_rows, int xmode) {
   using namespace annb;
   if (n <= 0 || chunk_rows <= 0) return;
   const int ld = (int)ann_big_ld(m);
@@ -358,6 +580,16 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
       const int nCB = (NT + ntb - 1) / ntb, BW = nCB < 8 ? nCB : 8, BH = 64 / BW;
       const int64_t groups = (nRB + BH - 1) / BH * ((nCB + BW - 1) / BW);
       const dim3 grid((unsigned)((groups + 7) / 8 * 8 * BH * BW));
+      if (xmode != IK_ANN_FP32 && L.wx && NT > 1 && lda % 32 == 0) {
+        // bf16x6 (the layer's split planes exist: a hidden layer after the first)
+        kt_begin("annb_gemm_x6_kernel", st);
+        hipLaunchKernelGGL(annb_gemm_x6_kernel, grid, dim3(256), 0, st, buf[cur], lda, rows,
+                           L.wx, lda / 32, L.np, L.bias, L.act, buf[cur ^ 1], L.np);
+        kt_end(st);
+        cur ^= 1;
+        lda = L.np;
+        continue;
+      }
       kt_begin("annb_gemm_kernel", st);
       if (NT == 1)
         hipLaunchKernelGGL(annb_gemm_kernel<1>, grid, dim3(256), 0, st, buf[cur], lda, rows,

@@ -214,8 +214,10 @@ int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bo
       IK_HIP(hipMalloc(&c->ann_act, bytes));
       c->ann_act_bytes = bytes;
     }
+    // (both split modes run bf16x6 here: fp16x3's bounded-input planes are the
+    // fused kernel's)
     launch_ann_big(c->ann_bigm, c->robot, dp, n, da, de, limits, S, c->stream,
-                   static_cast<float *>(c->ann_act), rows);
+                   static_cast<float *>(c->ann_act), rows, c->ann_mode);
     IK_HIP(hipGetLastError());
     return IK_OK;
   }
@@ -731,13 +733,17 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   // single-column-tile output layer) -- the split bf16 planes
   std::vector<size_t> woff(n_layers), boff(n_layers), xoff(n_layers, 0), hoff(n_layers, 0);
   std::vector<int> hexp(n_layers, 0);
-  // models wider than 512 run the wide fp32 kernel only: no split operands
+  // models wider than 512 run the wide fp32 kernel only: no split operands; the
+  // layered path (big) has its own bf16x6 planes (ann_big_pack_x)
   bool wide = big;
   for (int l = 0; l <= n_layers; ++l) wide = wide || dims[l] > 512;
-  auto splittable = [&](int l) { return !wide && l > 0 && (dims[l + 1] + 31) / 32 > 1; };
+  auto splittable = [&](int l) {
+    return (!wide || big) && l > 0 && (dims[l + 1] + 31) / 32 > 1;
+  };
   // fp16x3 also needs a bounded layer input: the layer before is tanh or sigmoid
   auto halvable = [&](int l) {
-    return splittable(l) && (acts[l - 1] == IK_ACT_TANH || acts[l - 1] == IK_ACT_SIGMOID);
+    return !big && splittable(l) &&
+           (acts[l - 1] == IK_ACT_TANH || acts[l - 1] == IK_ACT_SIGMOID);
   };
   size_t total = 0;
   for (int l = 0; l < n_layers; ++l) {
@@ -784,7 +790,10 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
       char *h = host.data();  // the section starts at woff[l] in the model buffer
       ann_pack_layer(W[l], dims[l], dims[l + 1], reinterpret_cast<float *>(h));
       std::memcpy(h + (boff[l] - woff[l]), b[l], (size_t)dims[l + 1] * 4);
-      if (splittable(l)) ann_pack_layer_x(W[l], dims[l], dims[l + 1], h + (xoff[l] - woff[l]));
+      if (splittable(l)) {
+        if (big) ann_big_pack_x(W[l], dims[l], dims[l + 1], h + (xoff[l] - woff[l]));
+        else ann_pack_layer_x(W[l], dims[l], dims[l + 1], h + (xoff[l] - woff[l]));
+      }
       if (halvable(l)) {
         hexp[l] = ann_h_scale_exp(W[l], dims[l], dims[l + 1]);
         ann_pack_layer_h(W[l], dims[l], dims[l + 1], hexp[l], h + (hoff[l] - woff[l]));
@@ -803,7 +812,9 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
     for (int l = 0; l < n_layers; ++l)
       bm.layers.push_back({(dims[l] + 7) / 8 * 8, (dims[l + 1] + 31) / 32 * 32, acts[l],
                            reinterpret_cast<const float *>(base + woff[l]),
-                           reinterpret_cast<const float *>(base + boff[l])});
+                           reinterpret_cast<const float *>(base + boff[l]),
+                           splittable(l) ? reinterpret_cast<const uint16_t *>(base + xoff[l])
+                                         : nullptr});
     for (int i = 0; i < 3; ++i) {
       bm.xm[i] = x_mean[i];
       bm.xs[i] = x_scale[i];

@@ -584,6 +584,7 @@ struct AnnBigLayer {
   int kp, np, act;   // padded in-dim (multiple of 8), padded out-dim (multiple of 32)
   const float *wp;   // packed weights (ann_pack_layer order)
   const float *bias; // np floats, zero past the layer's width
+  const uint16_t *wx = nullptr;  // bf16x6 planes (ann_big_pack_x), hidden layers only
 };
 struct AnnBigModel {
   std::vector<AnnBigLayer> layers;
@@ -591,10 +592,13 @@ struct AnnBigModel {
 };
 // floats per activation row (the widest padded layer, at least 8)
 size_t ann_big_ld(const AnnBigModel &m);
+// the layered path's bf16x6 weight planes: [plane][ceil(k / 32)][np][32] bf16
+// (ann_x_bytes(k, n) bytes)
+void ann_big_pack_x(const float *W, int k, int n, void *dst);
 // rows per chunk that fit two activation buffers in act_bytes (multiple of 128)
 int64_t ann_big_rows(const AnnBigModel &m, size_t act_bytes);
 // act: 2 * chunk_rows * ann_big_ld(m) floats
 void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, int64_t n,
                     float *ang, double *fk_err, bool check_limits, DevStats *S, hipStream_t st,
-                    float *act, int64_t chunk_rows);
+                    float *act, int64_t chunk_rows, int xmode = 0);
 }  // namespace ikhip

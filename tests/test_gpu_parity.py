@@ -429,6 +429,10 @@ def test_ann_width_cap(ctx1):
     ((3, 512, 512, 4), "relu"),                 # fp16x3: unbounded input -> fp32 layer
     ((3, 96, 96, 4), "sigmoid"),
     ((3, 64, 32, 64, 4), "tanh"),               # a split-K (32-wide) layer feeds a split one
+    # the layered path (annb_gemm_x6_kernel; fp16x3 runs bf16x6 there)
+    ((3, 2048, 2048, 4), "tanh"),
+    ((3,) + (64,) * 29 + (4,), "tanh"),
+    ((3, 1100, 200, 37, 4), "relu"),            # partial 128-feature tiles, K of 1120 / 224
 ])
 def test_ann_split_modes(ctx1, dims, act, mode):
     """IK_ANN_BF16X6 / IK_ANN_FP16X3: split hidden GEMMs stay within the
@@ -447,6 +451,27 @@ def test_ann_split_modes(ctx1, dims, act, mode):
     print(f"{mode} {dims[:3]}.. {act}: max|d| {d_x:.3e} (fp32 mode {d_f:.3e})")
     assert d_x <= NS_TOL, d_x             # north_star: 1e-5 absolute
     assert d_x <= 4 * d_f + 2e-7, (d_x, d_f)
+
+
+def test_ann_layered_bf16x6_kernel_runs(ctx1):
+    """In a split mode the layered path's hidden layers after the first run the
+    bf16x6 GEMM (annb_gemm_x6_kernel) and the first / output layers the fp32 one;
+    in fp32 mode only the fp32 one runs."""
+    dims = (3, 1100, 300, 4)
+    names = {}
+    for mode in ("fp32", "bf16x6"):
+        try:
+            ctx1.ann_set_mode(mode)
+            ctx1.set_timing(True)
+            _ann_case(ctx1, dims, "tanh", 1000, seed=2)
+            names[mode] = [k for k, _ in ctx1.kernel_times()]
+        finally:
+            ctx1.set_timing(False)
+            ctx1.ann_set_mode("fp32")
+    assert names["fp32"].count("annb_gemm_kernel") == 3
+    assert "annb_gemm_x6_kernel" not in names["fp32"]
+    assert names["bf16x6"].count("annb_gemm_x6_kernel") == 1
+    assert names["bf16x6"].count("annb_gemm_kernel") == 2
 
 
 def test_ann_fp16x3_layer_mix(ctx1):

@@ -3,7 +3,8 @@ csrc/ik_ann_big.hip): a few model shapes on n random_dist points, device arrays,
 per-kernel HIP-event times of one call and the mean of `reps` calls; prints one JSON
 line per model with the achieved TFLOP/s of the Dense layers (2 * sum in * out per point).
 
-    python tools/ann_big_probe.py [n] [only]   (only: e.g. 4096x2, one model)
+    python tools/ann_big_probe.py [n] [only] [mode]   (only: e.g. 4096x2 or "all";
+                                                      mode: fp32 (default) / bf16x6)
 """
 import json
 import os
@@ -23,7 +24,9 @@ def main():
     ctx = _native.Context(0)
     pts = torch.from_numpy(random_dist(n, seed=0)).cuda()
     ang = torch.empty((n, 4), dtype=torch.float32, device="cuda")
-    only = sys.argv[2] if len(sys.argv) > 2 else None
+    only = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "all" else None
+    mode = sys.argv[3] if len(sys.argv) > 3 else "fp32"
+    ctx.ann_set_mode(mode)
     for dims in ((3, 2048, 2048, 4), (3,) + (512,) * 30 + (4,), (3, 4096, 4096, 4),
                  (3,) + (500,) * 12 + (4,)):
         if only and only != f"{dims[1]}x{len(dims) - 2}":
@@ -46,7 +49,8 @@ def main():
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / reps
         gemm = sum(v for k, v in ks if "gemm" in k)
-        print(json.dumps({"dims": f"{dims[1]}x{len(dims) - 2}", "points": n, "ms_per_call": ms,
+        print(json.dumps({"dims": f"{dims[1]}x{len(dims) - 2}", "mode": mode, "points": n,
+                          "ms_per_call": ms,
                           "tflops_call": flop / ms / 1e9,
                           "gemm_ms_events": gemm, "tflops_gemm": flop / gemm / 1e9 if gemm else None,
                           "kernels": len(ks)}), flush=True)
