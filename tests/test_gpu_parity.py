@@ -474,6 +474,22 @@ def test_ann_layered_bf16x6_kernel_runs(ctx1):
     assert names["bf16x6"].count("annb_gemm_kernel") == 2
 
 
+def test_ann_layered_bf16x6_chunks(ctx1, monkeypatch):
+    """bf16x6 through the layered path over many chunks (a 1 MiB activation budget;
+    the buffers hold three bf16 planes per element between split layers) equals one
+    chunk bit for bit and stays within 1e-5 of a float64 forward."""
+    dims = (3, 1100, 300, 200, 4)
+    try:
+        ctx1.ann_set_mode("bf16x6")
+        _, pts, ang1, _, _, ref64 = _ann_case(ctx1, dims, "tanh", 3000, seed=9)
+        monkeypatch.setenv("IKHIP_ANN_ACT_MB", "1")
+        ang2, _, _ = ctx1.ann_solve(pts, check_limits=False)
+    finally:
+        ctx1.ann_set_mode("fp32")
+    assert np.array_equal(ang1, ang2)
+    assert np.abs(ang2.astype(np.float64) - ref64).max() <= NS_TOL
+
+
 def test_ann_fp16x3_layer_mix(ctx1):
     """fp16x3 on a model whose layers switch between the split GEMM (input bounded:
     after tanh / sigmoid) and fp32 (after relu / linear, or 32-wide split-K layers),
