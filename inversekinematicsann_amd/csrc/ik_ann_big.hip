@@ -360,12 +360,15 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
 #pragma unroll
     for (int fm = 0; fm < 4; ++fm) acc[pm][fm] = (f32x4)(0.0f);
 
-  const uint32_t kOOB = 0x80000000u;
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float *>(A) + row0 * (int64_t)lda, 0,
       (int)((rows - row0 < kBM2 ? rows - row0 : kBM2) * (int64_t)lda * 4), 0x00020000);
+  // the planes' feature rows are padded to whole 128-feature blocks (zeros), so
+  // no load needs a range check: the prefetch past the last stage reads the next
+  // plane's first stage or past the end (zeros), and is never stored
+  const int NPp = (NP + 127) / 128 * 128;
   const auto rsW = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t *>(wx), 0, (int)((size_t)3 * KG * NP * 64), 0x00020000);
+      const_cast<uint16_t *>(wx), 0, (int)((size_t)3 * KG * NPp * 64), 0x00020000);
   // stage s: activations, 8 k of point (b >> 2) at k block (b & 3) for b = tid,
   // tid + 256 (two 16-byte loads each); weights, plane i >> 1, 16 bytes of feature
   // row (c >> 2) at k block (c & 3) for c = 256 (i & 1) + tid
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int bb = tid + 256 * i, p = bb >> 2, kb = bb & 3;
-      const uint32_t off = s < KG ? (uint32_t)((p * lda + s * 32 + 8 * kb) * 4) : kOOB;
+      const uint32_t off = (uint32_t)((p * lda + s * 32 + 8 * kb) * 4);
       ra[2 * i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
       ra[2 * i + 1] =
           __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off + 16, 0, 0));
@@ -381,9 +384,7 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
       const int c = 256 * (i & 1) + tid, n = c >> 2, kb = c & 3, pl = i >> 1;
-      const uint32_t off = (s < KG && n0 + n < NP)
-                               ? (uint32_t)(((((size_t)pl * KG + s) * NP + n0 + n) * 32 + 8 * kb) * 2)
-                               : kOOB;
+      const uint32_t off = (uint32_t)(((((size_t)pl * KG + s) * NPp + n0 + n) * 32 + 8 * kb) * 2);
       rw[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsW, off, 0, 0));
     }
   };
@@ -410,28 +411,36 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
     __syncthreads();  // the last stage's fragments are read
     store(ra, rw);
     __syncthreads();
-    load(ra, rw, s + 1);  // (past the last stage: out of range, zeros, never stored)
+    load(ra, rw, s + 1);  // (past the last stage: never stored)
+    // the loads go out first: their latency runs under this stage's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
     bf16x8 xf[4][3];
 #pragma unroll
     for (int pm = 0; pm < 4; ++pm)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
         xf[pm][pl] = *reinterpret_cast<const bf16x8 *>(&Xs[pl][xoff(wm * 64 + pm * 16 + fr, fkb)]);
-#pragma unroll
-    for (int fm = 0; fm < 4; ++fm) {
-      bf16x8 wf[3];
+    // the next feature subtile's weight fragments are read before this one's MFMAs
+    bf16x8 wf[2][3];
+    auto read_w = [&](bf16x8 (&w)[3], int fm) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        wf[pl] = *reinterpret_cast<const bf16x8 *>(&Ws[pl][xoff(wn * 64 + fm * 16 + fr, fkb)]);
+        w[pl] = *reinterpret_cast<const bf16x8 *>(&Ws[pl][xoff(wn * 64 + fm * 16 + fr, fkb)]);
+    };
+    read_w(wf[0], 0);
+#pragma unroll
+    for (int fm = 0; fm < 4; ++fm) {
+      if (fm < 3) read_w(wf[(fm + 1) & 1], fm + 1);
+      const bf16x8(&w)[3] = wf[fm & 1];
 #pragma unroll
       for (int pm = 0; pm < 4; ++pm) {
         f32x4 c = acc[pm][fm];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], xf[pm][2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], xf[pm][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[2], xf[pm][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], xf[pm][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[1], xf[pm][0], c, 0, 0, 0);
-        acc[pm][fm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[0], xf[pm][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xf[pm][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xf[pm][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[2], xf[pm][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xf[pm][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[1], xf[pm][0], c, 0, 0, 0);
+        acc[pm][fm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xf[pm][0], c, 0, 0, 0);
       }
     }
   }
@@ -536,8 +545,12 @@ static float bf16_f32_h(uint16_t h) {
   return x;
 }
 
+size_t ann_big_x_bytes(int k, int n) {
+  return (size_t)3 * ((k + 31) / 32) * ((n + 127) / 128 * 128) * 32 * 2;
+}
+
 void ann_big_pack_x(const float *W, int k, int n, void *dst) {
-  const int KG = (k + 31) / 32, NP = (n + 31) / 32 * 32;
+  const int KG = (k + 31) / 32, NP = (n + 127) / 128 * 128;  // (whole 128-feature blocks)
   uint16_t *d = static_cast<uint16_t *>(dst);
   const size_t plane = (size_t)KG * NP * 32;
   for (int g = 0; g < KG; ++g)

@@ -755,7 +755,7 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
     total = (total + 255) & ~(size_t)255;
     if (splittable(l)) {
       xoff[l] = total;
-      total += ann_x_bytes(dims[l], dims[l + 1]);
+      total += big ? ann_big_x_bytes(dims[l], dims[l + 1]) : ann_x_bytes(dims[l], dims[l + 1]);
       total = (total + 255) & ~(size_t)255;
     }
     if (halvable(l)) {

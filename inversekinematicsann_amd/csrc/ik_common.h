@@ -592,8 +592,9 @@ struct AnnBigModel {
 };
 // floats per activation row (the widest padded layer, at least 8)
 size_t ann_big_ld(const AnnBigModel &m);
-// the layered path's bf16x6 weight planes: [plane][ceil(k / 32)][np][32] bf16
-// (ann_x_bytes(k, n) bytes)
+// the layered path's bf16x6 weight planes: [plane][ceil(k / 32)][n rounded up to
+// 128][32] bf16, ann_big_x_bytes(k, n) bytes
+size_t ann_big_x_bytes(int k, int n);
 void ann_big_pack_x(const float *W, int k, int n, void *dst);
 // rows per chunk that fit two activation buffers in act_bytes (multiple of 128)
 int64_t ann_big_rows(const AnnBigModel &m, size_t act_bytes);
