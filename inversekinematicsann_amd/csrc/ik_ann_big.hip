@@ -289,15 +289,15 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_kernel(const float *__restri
 // v_mfma_f32_16x16x32_bf16 (exact bf16 products): fp32-level results at 6 bf16
 // MFMAs (96 cycles) per 16 x 16 x 32 block instead of 16 fp32 ones (256).
 //
-// Tile 128 points x 128 features, 4 waves of 64 x 64 (4 x 4 accumulators of 16 x
-// 16), two workgroups per CU.  The weights are the MFMA's A operand (16 features
-// x 32 k) and the activations its B operand (32 k x 16 points), so a lane's
-// accumulator holds 4 consecutive features of one point: one 16-byte store.
-// Stages of 32 in K through LDS (one buffer each for the activations' and the
-// weights' three planes, 48 KiB): the activations arrive fp32 from HBM and are
-// split as they are written to LDS, the weights arrive split (ann_big_pack_x:
-// [plane][K / 32][features][32] bf16).  The next stage's loads are issued
-// before the current stage's MFMAs, into registers.
+// Tile 256 points x 128 features, 8 waves of 64 x 64 (4 x 4 accumulators of 16 x
+// 16), one workgroup per CU (two waves per SIMD).  The weights are the MFMA's A
+// operand (16 features x 32 k) and the activations its B operand (32 k x 16
+// points), so a lane's accumulator holds 4 consecutive features of one point: one
+// 16-byte store.  Stages of 32 in K, double-buffered through LDS (activations and
+// weights, three planes each, 2 x 72 KiB), one barrier per stage: the activations
+// arrive fp32 from HBM and are split as they are written to LDS, the weights arrive
+// split (ann_big_pack_x: [plane][K / 32][features][32] bf16).  (A 128 x 128 tile with
+// one LDS buffer, two barriers a stage and two workgroups per CU: MFMA busy 58 %.)
 // LDS rows of 32 bf16 (64 B), the 16-byte block kb of row r at position
 // kb ^ (2 ((r >> 3) & 1)): each of ds_read_b128's four 16-lane groups ({0-3, 12-15,
 // 20-27}, {4-11, 16-19, 28-31}, and the same + 32; MI355X_MICROARCH.md "LDS") then
@@ -333,17 +333,19 @@ __device__ __forceinline__ Split3 split3(f32x4 a, f32x4 b) {
           __builtin_bit_cast(bf16x8, l)};
 }
 
-__global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
+constexpr int kBMX = 256;  // bf16x6 tile: points per workgroup
+__global__ __launch_bounds__(512, 1) void annb_gemm_x6_kernel(
     const float *__restrict__ A, int lda, int64_t rows, const uint16_t *__restrict__ wx, int KG,
     int NP, const float *__restrict__ bias, int act, float *__restrict__ C, int ldc) {
-  __shared__ __attribute__((aligned(16))) uint16_t Xs[3][kBM2 * 32];  // 3 x 8 KiB
-  __shared__ __attribute__((aligned(16))) uint16_t Ws[3][kBM2 * 32];  // 3 x 8 KiB
+  // two stages: [stage][plane][rows x 32 bf16]; 96 + 48 KiB
+  __shared__ __attribute__((aligned(16))) uint16_t Xs[2][3][kBMX * 32];
+  __shared__ __attribute__((aligned(16))) uint16_t Ws[2][3][128 * 32];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves of 64 points x 64 features
+  const int wm = wave >> 1, wn = wave & 1;  // 4 x 2 waves of 64 points x 64 features
   // the fp32 kernel's XCD-aware 2-D tile groups (128 features = 4 column tiles)
   const int NT = NP / 32;
   const int nCB = (NT + 3) / 4;
-  const int64_t nRB = (rows + kBM2 - 1) / kBM2;
+  const int64_t nRB = (rows + kBMX - 1) / kBMX;
   const int BW = nCB < 8 ? nCB : 8, BH = 64 / BW, per = BH * BW;
   const int nBC = (nCB + BW - 1) / BW;
   const unsigned b = blockIdx.x, xcd = b & 7u, kx = b >> 3;
@@ -352,7 +354,8 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
   const int64_t rb = (grp / nBC) * BH + inb / BW;
   const int cb = (int)(grp % nBC) * BW + inb % BW;
   if (rb >= nRB || cb >= nCB) return;  // the grid is padded to whole groups
-  const int64_t row0 = rb * kBM2;
+  const int64_t row0 = rb * kBMX;
+  const int vrows = (int)(rows - row0 < kBMX ? rows - row0 : kBMX);
   const int n0 = cb * 128;  // the block's first feature
   f32x4 acc[4][4];          // [point subtile][feature subtile]
 #pragma unroll
@@ -361,71 +364,60 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
     for (int fm = 0; fm < 4; ++fm) acc[pm][fm] = (f32x4)(0.0f);
 
   const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<float *>(A) + row0 * (int64_t)lda, 0,
-      (int)((rows - row0 < kBM2 ? rows - row0 : kBM2) * (int64_t)lda * 4), 0x00020000);
+      const_cast<float *>(A) + row0 * (int64_t)lda, 0, (int)(vrows * (int64_t)lda * 4), 0x00020000);
   // the planes' feature rows are padded to whole 128-feature blocks (zeros), so
-  // no load needs a range check: the prefetch past the last stage reads the next
-  // plane's first stage or past the end (zeros), and is never stored
+  // no load needs a range check: a prefetch past the last stage reads the next
+  // plane's stages, the next rows or past the end (zeros), and is never read back
   const int NPp = (NP + 127) / 128 * 128;
   const auto rsW = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t *>(wx), 0, (int)((size_t)3 * KG * NPp * 64), 0x00020000);
   // stage s: activations, 8 k of point (b >> 2) at k block (b & 3) for b = tid,
-  // tid + 256 (two 16-byte loads each); weights, plane i >> 1, 16 bytes of feature
-  // row (c >> 2) at k block (c & 3) for c = 256 (i & 1) + tid
-  auto load = [&](f32x4 (&ra)[4], u32x4 (&rw)[6], int s) {
+  // tid + 512 (two 16-byte loads each); weights, plane i, 16 bytes of feature row
+  // (tid >> 2) at k block (tid & 3)
+  auto load = [&](f32x4 (&ra)[4], u32x4 (&rw)[3], int s) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int bb = tid + 256 * i, p = bb >> 2, kb = bb & 3;
+      const int bb = tid + 512 * i, p = bb >> 2, kb = bb & 3;
       const uint32_t off = (uint32_t)((p * lda + s * 32 + 8 * kb) * 4);
       ra[2 * i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off, 0, 0));
       ra[2 * i + 1] =
           __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsA, off + 16, 0, 0));
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int c = 256 * (i & 1) + tid, n = c >> 2, kb = c & 3, pl = i >> 1;
+    for (int pl = 0; pl < 3; ++pl) {
+      const int n = tid >> 2, kb = tid & 3;
       const uint32_t off = (uint32_t)(((((size_t)pl * KG + s) * NPp + n0 + n) * 32 + 8 * kb) * 2);
-      rw[i] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsW, off, 0, 0));
+      rw[pl] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsW, off, 0, 0));
     }
   };
-  auto store = [&](const f32x4 (&ra)[4], const u32x4 (&rw)[6]) {
+  auto store = [&](const f32x4 (&ra)[4], const u32x4 (&rw)[3], int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int bb = tid + 256 * i, p = bb >> 2, kb = bb & 3;
+      const int bb = tid + 512 * i, p = bb >> 2, kb = bb & 3;
       const Split3 x = split3(ra[2 * i], ra[2 * i + 1]);
-      *reinterpret_cast<bf16x8 *>(&Xs[0][xoff(p, kb)]) = x.hi;
-      *reinterpret_cast<bf16x8 *>(&Xs[1][xoff(p, kb)]) = x.mid;
-      *reinterpret_cast<bf16x8 *>(&Xs[2][xoff(p, kb)]) = x.lo;
+      *reinterpret_cast<bf16x8 *>(&Xs[buf][0][xoff(p, kb)]) = x.hi;
+      *reinterpret_cast<bf16x8 *>(&Xs[buf][1][xoff(p, kb)]) = x.mid;
+      *reinterpret_cast<bf16x8 *>(&Xs[buf][2][xoff(p, kb)]) = x.lo;
     }
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int c = 256 * (i & 1) + tid, n = c >> 2, kb = c & 3, pl = i >> 1;
-      *reinterpret_cast<u32x4 *>(&Ws[pl][xoff(n, kb)]) = rw[i];
-    }
+    for (int pl = 0; pl < 3; ++pl)
+      *reinterpret_cast<u32x4 *>(&Ws[buf][pl][xoff(tid >> 2, tid & 3)]) = rw[pl];
   };
   const int fr = lane & 15, fkb = lane >> 4;
-  f32x4 ra[4];
-  u32x4 rw[6];
-  load(ra, rw, 0);
-  for (int s = 0; s < KG; ++s) {
-    __syncthreads();  // the last stage's fragments are read
-    store(ra, rw);
-    __syncthreads();
-    load(ra, rw, s + 1);  // (past the last stage: never stored)
-    // the loads go out first: their latency runs under this stage's MFMAs
-    __builtin_amdgcn_sched_barrier(0);
+  auto compute = [&](int buf) {
     bf16x8 xf[4][3];
 #pragma unroll
     for (int pm = 0; pm < 4; ++pm)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        xf[pm][pl] = *reinterpret_cast<const bf16x8 *>(&Xs[pl][xoff(wm * 64 + pm * 16 + fr, fkb)]);
+        xf[pm][pl] =
+            *reinterpret_cast<const bf16x8 *>(&Xs[buf][pl][xoff(wm * 64 + pm * 16 + fr, fkb)]);
     // the next feature subtile's weight fragments are read before this one's MFMAs
     bf16x8 wf[2][3];
     auto read_w = [&](bf16x8 (&w)[3], int fm) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        w[pl] = *reinterpret_cast<const bf16x8 *>(&Ws[pl][xoff(wn * 64 + fm * 16 + fr, fkb)]);
+        w[pl] = *reinterpret_cast<const bf16x8 *>(&Ws[buf][pl][xoff(wn * 64 + fm * 16 + fr, fkb)]);
     };
     read_w(wf[0], 0);
 #pragma unroll
@@ -443,12 +435,27 @@ __global__ __launch_bounds__(256, 2) void annb_gemm_x6_kernel(
         acc[pm][fm] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[0], xf[pm][0], c, 0, 0, 0);
       }
     }
+  };
+  // double-buffered stages, one barrier each: at stage s the registers hold stage
+  // s + 1 (loaded a stage ago), which goes to the other buffer (last read at stage
+  // s - 1, before the barrier), stage s + 2's loads go out, then stage s's MFMAs
+  f32x4 ra[4];
+  u32x4 rw[3];
+  load(ra, rw, 0);
+  store(ra, rw, 0);
+  load(ra, rw, 1);
+  __syncthreads();
+  for (int s = 0; s < KG; ++s) {
+    store(ra, rw, (s + 1) & 1);  // (past the last stage: never read)
+    load(ra, rw, s + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(s & 1);
+    __syncthreads();
   }
   // bias + activation: lane (fr, lane >> 4) of accumulator (pm, fm) holds features
   // 4 (lane >> 4) .. + 3 of feature subtile fm for point fr of point subtile pm
   const auto rsC = __builtin_amdgcn_make_buffer_rsrc(
-      C + row0 * (int64_t)ldc, 0,
-      (int)((rows - row0 < kBM2 ? rows - row0 : kBM2) * (int64_t)ldc * 4), 0x00020000);
+      C + row0 * (int64_t)ldc, 0, (int)(vrows * (int64_t)ldc * 4), 0x00020000);
   auto epilogue = [&](auto actc) {
     constexpr int ACT = decltype(actc)::value;
 #pragma unroll
@@ -600,9 +607,13 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
       const int64_t groups = (nRB + BH - 1) / BH * ((nCB + BW - 1) / BW);
       const dim3 grid((unsigned)((groups + 7) / 8 * 8 * BH * BW));
       if (xmode != IK_ANN_FP32 && L.wx && NT > 1 && lda % 32 == 0) {
-        // bf16x6 (the layer's split planes exist: a hidden layer after the first)
+        // bf16x6 (the layer's split planes exist: a hidden layer after the first),
+        // 256-row tiles of 512 threads
+        const int64_t xRB = (rows + kBMX - 1) / kBMX;
+        const int64_t xgroups = (xRB + BH - 1) / BH * ((nCB + BW - 1) / BW);
+        const dim3 xgrid((unsigned)((xgroups + 7) / 8 * 8 * BH * BW));
         kt_begin("annb_gemm_x6_kernel", st);
-        hipLaunchKernelGGL(annb_gemm_x6_kernel, grid, dim3(256), 0, st, buf[cur], lda, rows,
+        hipLaunchKernelGGL(annb_gemm_x6_kernel, xgrid, dim3(512), 0, st, buf[cur], lda, rows,
                            L.wx, lda / 32, L.np, L.bias, L.act, buf[cur ^ 1], L.np);
         kt_end(st);
         cur ^= 1;
