@@ -182,7 +182,9 @@ int ik_ann_solve(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *
  * pre-scaled by a power of two) and three fp16 MFMA products, on layers whose
  * input is tanh/sigmoid-bounded (others stay fp32); as close to a float64
  * forward as numpy's float32 one on the tested networks, at ~5x the MFMA rate.
- * The input layer and a one-tile output layer stay fp32 in every mode.
+ * The input layer and a one-tile output layer stay fp32 in every mode.  Models
+ * wider than 512 on the fused kernel stay fp32; models past its caps (the
+ * layered path) run bf16x6 in either split mode.
  * Environment default: IKHIP_ANN_MODE=bf16x6|fp16x3. */
 enum { IK_ANN_FP32 = 0, IK_ANN_BF16X6 = 1, IK_ANN_FP16X3 = 2 };
 int ik_ann_set_mode(ik_ctx *ctx, int mode);
