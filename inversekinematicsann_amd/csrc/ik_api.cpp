@@ -737,8 +737,9 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   // layered path (big) has its own bf16x6 planes (ann_big_pack_x)
   bool wide = big;
   for (int l = 0; l <= n_layers; ++l) wide = wide || dims[l] > 512;
+  bool planes = true;  // (dropped below when only the fp32 operands fit the device)
   auto splittable = [&](int l) {
-    return (!wide || big) && l > 0 && (dims[l + 1] + 31) / 32 > 1;
+    return planes && (!wide || big) && l > 0 && (dims[l + 1] + 31) / 32 > 1;
   };
   // fp16x3 also needs a bounded layer input: the layer before is tanh or sigmoid
   auto halvable = [&](int l) {
@@ -746,24 +747,28 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
            (acts[l - 1] == IK_ACT_TANH || acts[l - 1] == IK_ACT_SIGMOID);
   };
   size_t total = 0;
-  for (int l = 0; l < n_layers; ++l) {
-    woff[l] = total;
-    total += ann_packed_floats(dims[l], dims[l + 1]) * 4;
-    total = (total + 255) & ~(size_t)255;
-    boff[l] = total;
-    total += (size_t)((dims[l + 1] + 31) / 32 * 32) * 4;
-    total = (total + 255) & ~(size_t)255;
-    if (splittable(l)) {
-      xoff[l] = total;
-      total += big ? ann_big_x_bytes(dims[l], dims[l + 1]) : ann_x_bytes(dims[l], dims[l + 1]);
+  auto layout = [&]() {
+    total = 0;
+    for (int l = 0; l < n_layers; ++l) {
+      woff[l] = total;
+      total += ann_packed_floats(dims[l], dims[l + 1]) * 4;
       total = (total + 255) & ~(size_t)255;
-    }
-    if (halvable(l)) {
-      hoff[l] = total;
-      total += ann_h_bytes(dims[l], dims[l + 1]);
+      boff[l] = total;
+      total += (size_t)((dims[l + 1] + 31) / 32 * 32) * 4;
       total = (total + 255) & ~(size_t)255;
+      if (splittable(l)) {
+        xoff[l] = total;
+        total += big ? ann_big_x_bytes(dims[l], dims[l + 1]) : ann_x_bytes(dims[l], dims[l + 1]);
+        total = (total + 255) & ~(size_t)255;
+      }
+      if (halvable(l)) {
+        hoff[l] = total;
+        total += ann_h_bytes(dims[l], dims[l + 1]);
+        total = (total + 255) & ~(size_t)255;
+      }
     }
-  }
+  };
+  layout();
   // (the widths and depth are capped above, so `total` stays far below 2^64: at
   // most 4096 layers of a 16384 x 16384 product, ~4.4 TB -- but that may not fit
   // the device, and the host staging must not be one buffer of that size)
@@ -773,6 +778,10 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   c->ann_loaded = false;
   size_t dev_free = 0, dev_total = 0;
   IK_HIP(hipMemGetInfo(&dev_free, &dev_total));
+  if (total > dev_free) {  // without the split planes (the split modes then run fp32)?
+    planes = false;
+    layout();
+  }
   if (total > dev_free)
     return fail(IK_E_HIP, "ik_ann_load: the packed model needs " + std::to_string(total) +
                               " bytes of device memory, " + std::to_string(dev_free) +
