@@ -577,7 +577,7 @@ void launch_ann_wide(const AnnModelDev &m, const RobotDev &r, const double *pts,
 
 // Models outside the fused kernel's caps (more than kAnnMaxLayers layers or a
 // layer wider than kAnnMaxWidth): layer at a time through HBM (ik_ann_big.hip),
-// fp32 only.  Bounds of that path:
+// fp32, or bf16x6 for the hidden layers after the first in a split mode.  Bounds:
 constexpr int kAnnBigMaxLayers = 4096;
 constexpr int kAnnBigMaxWidth = 16384;
 struct AnnBigLayer {
