@@ -102,24 +102,27 @@ namespace ikhip {
 // fabrik.py:57-64 continues while se > tol or ge > tol, se = |B0 - start| and
 // ge = |F3 - goal| (squared here, against tol2).  With q = L0 / |b1 - start| the
 // start error is |(q - 1) (start - b1)| up to roundings, and with the carried
-// quotient cq the goal error is |(cq - 1) (goal - c2)|: se2a = (1 - q)^2 x and
-// ge2a = (1 - cq)^2 x3 from the radicands the step computes anyway.  The
+// quotient cq the goal error is |(cq - 1) (goal - c2)|: sea = |1 - q| sqrt(x) and
+// gea = |1 - cq| sqrt(x3) from the roots the step computes anyway.  The
 // reference's own se2 / ge2 (b0, F3 = c3 and their differences, 25 VALU) are
-// computed only when an approximation falls inside the lane's band [lo, hi]
+// computed only when an approximation falls inside the launch's band [lo, hi]
 // (ErrBand): outside it the comparison with tol2 provably comes out the same.
 //
-// The band (band_for): with u = 2^-53, every rounding of b0 = b1 + q (start - b1),
-// B0 - start and of the squares moves |B0 - start| by at most
+// The band: with u = 2^-53, every rounding of b0 = b1 + q (start - b1), B0 - start,
+// the squares and the root moves |B0 - start| by at most
 //   D <= 1.03 u (3 |goal| + 2 |start| + 3 sum L)
 // (the backward points lie within sum L of the goal, the forward ones within sum L
 // of the start; the same bound with the roles swapped covers the goal error), and
-// the relative errors of se2a and se2 are below 8u and 3u.  With T = sqrt(tol2):
-//   se2a > hi = (D + T)^2 (1 + 2^-36)        =>  se2 > tol2
-//   se2a < lo = (T - D)^2 (1 - 2^-36)        =>  se2 <= tol2   (only if D <= T / 2)
-// The band is one per launch (fabrik_band on the host): D from a bound n1max on
-// |start|_1 + |goal|_1, D = 2u (3 n1max + 4 sum L + 1) (twice the bound; L1 norms
-// bound the Euclidean ones), with T's bounds tol_lo <= T <= tol_hi.  A lane past
-// n1max (or with a non-finite goal) carries bok = false: its comparisons are exact.
+// sea's own relative error (1 - q, the root, the product) is below 3u.  With
+// T = sqrt(tol2) (real):
+//   sea > hi = (D + T) (1 + 2^-36)        =>  se2 > tol2
+//   sea < lo = (T - D) (1 - 2^-36)        =>  se2 <= tol2   (only if D <= T / 2)
+// (tests/test_band_cpu.py checks the bound along real iterations: the gap stays
+// below 0.17 D.)  The band is one per launch (fabrik_band on the host): D from a
+// bound n1max on |start|_1 + |goal|_1, D = 2u (3 n1max + 4 sum L + 1) (twice the
+// bound; L1 norms bound the Euclidean ones), with T's bounds tol_lo <= T <= tol_hi.
+// A lane past n1max (or with a non-finite goal) carries bok = false: its
+// comparisons are exact.
 struct ErrBand {
   double lo, hi;
 };
@@ -130,10 +133,8 @@ __host__ __forceinline__ ErrBand fabrik_band(double tol2, double n1max, double s
   const double T = std::sqrt(tol2);
   const double tol_lo = T * (1.0 - 0x1p-50), tol_hi = T * (1.0 + 0x1p-50);
   const double d = 0x1p-52 * (3.0 * n1max + 4.0 * sum_l + 1.0);
-  const double h = d + tol_hi;
-  b.hi = (h * h) * (1.0 + 0x1p-36);
-  const double l = tol_lo - d;
-  b.lo = (d <= 0.5 * tol_lo) ? (l * l) * (1.0 - 0x1p-36) : -1.0;
+  b.hi = (d + tol_hi) * (1.0 + 0x1p-36);
+  b.lo = (d <= 0.5 * tol_lo) ? (tol_lo - d) * (1.0 - 0x1p-36) : -1.0;
   return b;
 }
 
@@ -152,16 +153,16 @@ __device__ __forceinline__ void fabrik_step4_lazy(const d3 start, d3 &c1, d3 &c2
   const double dx = start.x - b1.x, dy = start.y - b1.y, dz = start.z - b1.z;
   const double x = sq(dx) + sq(dy) + sq(dz);
   dom = max(dom, sqrt_core_dom(x));
-  const double q = div_core(L[0], sqrt_core(x));
+  const double sx = sqrt_core(x);
+  const double q = div_core(L[0], sx);
   const double qx = q * dx, qy = q * dy, qz = q * dz;
   // the decisions as lane masks (ballots of the compares): the band tests, the
   // merges with the exact results and the uncertainty are scalar-ALU operations
   const uint64_t ex = __builtin_amdgcn_read_exec();
   const uint64_t nbok = __builtin_amdgcn_ballot_w64(!bok);
-  const double t = 1.0 - q;
-  const double se2a = (t * t) * x;
-  uint64_t gt = __builtin_amdgcn_ballot_w64(se2a > band.hi);
-  uint64_t unc = (ex & ~(gt | __builtin_amdgcn_ballot_w64(se2a < band.lo))) | nbok;
+  const double sea = fabs(1.0 - q) * sx;  // |B0 - start| from the radicand's root
+  uint64_t gt = __builtin_amdgcn_ballot_w64(sea > band.hi);
+  uint64_t unc = (ex & ~(gt | __builtin_amdgcn_ballot_w64(sea < band.lo))) | nbok;
   if (__builtin_expect(unc != 0, 0)) {  // (a NaN is uncertain)
     const d3 b0 = {b1.x + qx, b1.y + qy, b1.z + qz};
     const double se2 = dist3_sq(b0, start);
@@ -173,14 +174,14 @@ __device__ __forceinline__ void fabrik_step4_lazy(const d3 start, d3 &c1, d3 &c2
   const double x3 = sq(ex3) + sq(ey3) + sq(ez3);
   cdom = sqrt_core_dom(x3);
   dom = max(dom, cdom);
-  cq = div_core(L[3], sqrt_core(x3));
+  const double sx3 = sqrt_core(x3);
+  cq = div_core(L[3], sx3);
   cd = {ex3, ey3, ez3};
-  const double t3 = 1.0 - cq;
-  const double ge2a = (t3 * t3) * x3;
-  uint64_t gt3 = __builtin_amdgcn_ballot_w64(ge2a > band.hi);
+  const double gea = fabs(1.0 - cq) * sx3;  // |F3 - goal|
+  uint64_t gt3 = __builtin_amdgcn_ballot_w64(gea > band.hi);
   // (the goal error only matters where the start error has not decided already)
   uint64_t unc3 =
-      ((ex & ~(gt3 | __builtin_amdgcn_ballot_w64(ge2a < band.lo))) | nbok) & ~gt;
+      ((ex & ~(gt3 | __builtin_amdgcn_ballot_w64(gea < band.lo))) | nbok) & ~gt;
   if (__builtin_expect(unc3 != 0, 0)) {
     const d3 c3 = {c2.x + (cq * ex3), c2.y + (cq * ey3), c2.z + (cq * ez3)};
     const double ge2 = dist3_sq(c3, g);

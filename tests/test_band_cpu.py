@@ -2,7 +2,7 @@
 fabrik_band), checked numerically on the CPU: along real FABRIK iterations (numpy
 float64, the reference's arithmetic: kinematics/point.py:25-45, fabrik.py:19-64),
 the start and goal errors the step approximates from its radicands,
-(1 - q)^2 x and (1 - cq)^2 x3, stay within the band's D of the reference's own
+|1 - q| sqrt(x) and |1 - cq| sqrt(x3), stay within the band's D of the reference's own
 |B0 - start| and |F3 - goal|, and the band's decisions agree with the exact
 comparison for thresholds placed right at the errors.  The GPU tests check the
 kernel bit for bit; this pins the bound the kernel's proof rests on, including the
@@ -26,8 +26,8 @@ def band(tol2, n1max, sum_l):
     T = np.sqrt(tol2)
     tlo, thi = T * (1.0 - 2.0 ** -50), T * (1.0 + 2.0 ** -50)
     d = 2.0 ** -52 * (3.0 * n1max + 4.0 * sum_l + 1.0)
-    hi = ((d + thi) ** 2) * (1.0 + 2.0 ** -36)
-    lo = ((tlo - d) ** 2) * (1.0 - 2.0 ** -36) if d <= 0.5 * tlo else -1.0
+    hi = (d + thi) * (1.0 + 2.0 ** -36)
+    lo = (tlo - d) * (1.0 - 2.0 ** -36) if d <= 0.5 * tlo else -1.0
     return lo, hi, d
 
 
@@ -73,7 +73,9 @@ def test_band_bounds_the_approximate_errors():
 def test_band_decisions_match_exact_comparisons():
     """Thresholds from 1e-6 relative down to one ulp around the errors themselves:
     wherever the band decides, it decides as the exact squared comparison does (and
-    the thresholds closest to the error are left to the exact comparison)."""
+    the thresholds closest to the error are left to the exact comparison).  The
+    approximation is the kernel's root-space one, |1 - q| sqrt(x), against the
+    un-squared band; the exact comparison is the squared one."""
     rng = np.random.default_rng(6)
     L = 2.0
     J, g = chains(4000, rng)
@@ -87,20 +89,20 @@ def test_band_decisions_match_exact_comparisons():
         b1, _, _ = pb(b2, c1, L)
         b0, x, q = pb(b1, start, L)
         se2 = ((b0 - start) ** 2).sum(1)
-        se2a = ((1.0 - q) * (1.0 - q)) * x
+        sea = np.abs(1.0 - q) * np.sqrt(x)
         c1, _, _ = pb(start, b1, L)
         c2, _, _ = pb(c1, b2, L)
         for k in range(0, len(se2), 97):
             ts = [se2[k] * f for f in facs] + [se2[k], np.nextafter(se2[k], 0),
-                                               np.nextafter(se2[k], 1), se2a[k]]
+                                               np.nextafter(se2[k], 1), sea[k] * sea[k]]
             for tol2 in ts:
                 if not (tol2 > 0 and np.isfinite(tol2)):
                     continue
                 lo, hi, _ = band(tol2, n1max, 4 * L)
-                if se2a[k] > hi:
+                if sea[k] > hi:
                     assert se2[k] > tol2
                     checked += 1
-                elif se2a[k] < lo:
+                elif sea[k] < lo:
                     assert se2[k] <= tol2
                     checked += 1
                 else:
