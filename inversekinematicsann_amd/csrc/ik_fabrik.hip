@@ -790,7 +790,11 @@ fabrik_iter_kernel(FabArgs a) {
   __syncthreads();
   int head = (int)(blockIdx.x % kQueueHeads);
   unsigned long long na = 0;
-  int64_t nperm = 0, ni = 0;
+  // (nperm as loaded, 32 bits, widened by the stage that uses it, and the goal as
+  // three separate loads: each lands in the register the preparation reads, so no
+  // copy waits for a load right after its issue)
+  int32_t nperm = 0;
+  int64_t ni = 0;
   d3 ng = {0, 0, 0};
   bool dry = false;   // the queue and the batch are exhausted
   int rcnt = 0;       // entries in the retire ring
@@ -886,7 +890,12 @@ fabrik_iter_kernel(FabArgs a) {
       };
       auto stage2 = [&]() {
         // the grab's chunk: head h's k-th is the queue's (k * kQueueHeads + h)-th
-        nbase = ((int64_t)__shfl(na, 0, 64) * kQueueHeads + head) * a.chunk;
+        // (lane 0's value read into SGPRs: a shuffle would leave the batch's count,
+        // cursor and the hand-out loop divergent in the compiler's eyes)
+        const uint64_t na0 =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(na >> 32), 0) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)na, 0);
+        nbase = ((int64_t)na0 * kQueueHeads + head) * a.chunk;
         if (nbase >= a.n) {  // this head is dry: on to one the block has not seen dry
           if (lane == 0) atomicOr(&dry_heads, 1u << head);
           const unsigned m =
@@ -906,86 +915,99 @@ fabrik_iter_kernel(FabArgs a) {
         }
         ncount = (int)min((int64_t)a.chunk, a.n - nbase);
         if (lane < ncount) {
-          nperm = ORD ? (int64_t)a.perm[nbase + lane] : nbase + lane;
+          if (ORD) nperm = a.perm[nbase + lane];
         }
         nstage = 2;
       };
       auto stage3 = [&]() {
         if (lane < ncount) {
-          ng = {a.pts[3 * nperm], a.pts[3 * nperm + 1], a.pts[3 * nperm + 2]};
-          ni = nperm;
+          const int64_t ip = ORD ? (int64_t)nperm : nbase + lane;
+          int64_t iy = 3 * ip + 1, iz = 3 * ip + 2;
+          asm volatile("" : "+v"(iy), "+v"(iz));  // (three loads, not a merged x4 + x2)
+          ng = {a.pts[3 * ip], a.pts[iy], a.pts[iz]};
+          ni = ip;
         }
         nstage = 3;
       };
-      if (nstage == 0 && pptr >= pcount - 24) stage1();
-      else if (nstage == 1 && pptr >= pcount - 16) stage2();
-      else if (nstage == 2 && pptr >= pcount - 8) stage3();
-      IKHIP_DT_ACC(kDiagStageTicks, kDiagTSub);
-      // hand prepared points to the free lanes, preparing batches as needed
+      // hand prepared points to the free lanes: first what the batch holds, then, if
+      // the batch runs out, from the next one.  Straight-line code with one call
+      // site per stage: each stage's loads land in the registers the next stage
+      // reads, with no merge copies that would wait for them right after issue.
       const bool wasfree = !active;
       const int rank = __popcll(freem & lt_mask);
-      int handed = 0;
-      while (handed < nfree) {
-        if (pptr >= pcount) {
-          IKHIP_DG(kDiagGrabs, 1);
-          IKHIP_DT(kDiagTDrain);  // (scratch slot: the preparation's start)
-          while (nstage >= 0 && nstage < 3) {  // (stage2 may send it back to 0)
-            if (nstage == 0) stage1();
-            else if (nstage == 1) stage2();
-            else stage3();
-          }
-          if (nstage < 0) break;
-          // prepare: limits check and seed pose of the batch, one entry per lane
-          pcount = ncount;
-          pptr = 0;
-          nstage = 0;
-          prio_raise();
-          if (lane < pcount) {
-            const RcConst k = opaque_rc(a.rc);
-            if (a.check_limits && outside_rc(k, ng))
-              atomicMin(&a.S->first_oob, (unsigned long long)ni);
-            d3 Js[4];
-            (void)seed_pose((const RobotConstDev *)k, ng, Js);
-            double2 *w = PB.w[lane];
-            w[0] = {Js[0].x, Js[0].y};
-            w[1] = {Js[0].z, Js[1].x};
-            w[2] = {Js[1].y, Js[1].z};
-            w[3] = {Js[2].x, Js[2].y};
-            w[4] = {Js[2].z, ng.x};
-            w[5] = {ng.y, ng.z};
-            w[6] = {__longlong_as_double(ni), 0.0};
-          }
+      const int avail = pcount - pptr;
+      const int take1 = min(nfree, avail);
+      const bool prep = nfree > avail;  // the batch runs out: prepare the next one
+      bool mine = wasfree && rank < take1;
+      auto take_entry = [&](int src) {
+        const double2 *w = PB.w[src];
+        const double2 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5];
+        J0 = {w0.x, w0.y, w1.x};
+        J1 = {w1.y, w2.x, w2.y};
+        J2 = {w3.x, w3.y, w4.x};
+        g = {w4.y, w5.x, w5.y};
+        out = __double_as_longlong(w[6].x);
+      };
+      // (read before a preparation overwrites the batch)
+      if (mine) take_entry(pptr + rank);
+      pptr += take1;
+      // the next batch's stages: while the batch is down to its last 24 / 16 / 8
+      // entries, one per refill (a stage consumes what the one before loaded, so the
+      // loads are long done); before a preparation, the stages still missing.  No
+      // loop: when stage 2 finds its head dry (back to stage 1 on another), the free
+      // lanes stay free, the inner loop returns at once and the next refill goes on.
+      bool more = true;
+      if (nstage == 0 && (prep || avail <= 24)) { stage1(); more = prep; }
+      if (more && nstage == 1 && (prep || avail <= 16)) { stage2(); more = prep; }
+      if (more && nstage == 2 && (prep || avail <= 8)) stage3();
+      IKHIP_DT_ACC(kDiagStageTicks, kDiagTSub);
+      if (prep && nstage == 3) {
+        IKHIP_DG(kDiagGrabs, 1);
+        IKHIP_DT(kDiagTDrain);  // (scratch slot: the preparation's start)
+        // prepare: limits check and seed pose of the batch, one entry per lane
+        pcount = ncount;
+        nstage = 0;
+        prio_raise();
+        if (lane < pcount) {
+          const RcConst k = opaque_rc(a.rc);
+          if (a.check_limits && outside_rc(k, ng))
+            atomicMin(&a.S->first_oob, (unsigned long long)ni);
+          d3 Js[4];
+          (void)seed_pose((const RobotConstDev *)k, ng, Js);
+          double2 *w = PB.w[lane];
+          w[0] = {Js[0].x, Js[0].y};
+          w[1] = {Js[0].z, Js[1].x};
+          w[2] = {Js[1].y, Js[1].z};
+          w[3] = {Js[2].x, Js[2].y};
+          w[4] = {Js[2].z, ng.x};
+          w[5] = {ng.y, ng.z};
+          w[6] = {__longlong_as_double(ni), 0.0};
+        }
 #ifdef IKHIP_DIAG
-          // (the seed's loads are consumed before the stamp)
-          __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the batch's LDS writes landed
+        // (the seed's loads are consumed before the stamp)
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the batch's LDS writes landed
 #endif
-          IKHIP_DT_ACC(kDiagPrepTicks, kDiagTDrain);
-          IKHIP_DT_ACC(kDiagTRefill, kDiagTDrain);  // (not refill time)
-        }
-        const int take = min(nfree - handed, pcount - pptr);
-        const bool mine = wasfree && rank >= handed && rank < handed + take;
-        const int src = mine ? pptr + (rank - handed) : lane;
+        IKHIP_DT_ACC(kDiagPrepTicks, kDiagTDrain);
+        IKHIP_DT_ACC(kDiagTRefill, kDiagTDrain);  // (not refill time)
+        // the rest of the free lanes from the new batch (a short last chunk may leave
+        // some free until the next refill)
+        const int take2 = min(nfree - take1, pcount);
+        const bool mine2 = wasfree && rank >= take1 && rank < take1 + take2;
         __builtin_amdgcn_wave_barrier();  // the batch's LDS writes before the reads
-        if (mine) {
-          const double2 *w = PB.w[src];
-          const double2 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5];
-          J0 = {w0.x, w0.y, w1.x};
-          J1 = {w1.y, w2.x, w2.y};
-          J2 = {w3.x, w3.y, w4.x};
-          g = {w4.y, w5.x, w5.y};
-          out = __double_as_longlong(w[6].x);
-          st = IK_OK;
-          cont = true;  // the loop's initial errors of 1.0 (fabrik.py:53-54) exceed tol
-          step = 0;
-          active = true;
-          if constexpr (CORE == 2) {
-            reuse_carry(J2, g, L[3], cq, cd, cdom);
-            bok = fabs(J0.x) + fabs(J0.y) + fabs(J0.z) + fabs(g.x) + fabs(g.y) + fabs(g.z) <=
-                  a.band_n1;
-          }
+        if (mine2) take_entry(rank - take1);
+        pptr = take2;
+        mine = mine || mine2;
+      }
+      if (mine) {
+        st = IK_OK;
+        cont = true;  // the loop's initial errors of 1.0 (fabrik.py:53-54) exceed tol
+        step = 0;
+        active = true;
+        if constexpr (CORE == 2) {
+          reuse_carry(J2, g, L[3], cq, cd, cdom);
+          bok = fabs(J0.x) + fabs(J0.y) + fabs(J0.z) + fabs(g.x) + fabs(g.y) + fabs(g.z) <=
+                a.band_n1;
         }
-        pptr += take;
-        handed += take;
       }
       dry = nstage < 0 && pptr >= pcount;
       IKHIP_DT_ACC(kDiagRefillTicks, kDiagTRefill);
