@@ -956,14 +956,16 @@ fabrik_iter_kernel(FabArgs a) {
       // loads are long done); before a preparation, the stages still missing.  No
       // loop: when stage 2 finds its head dry (back to stage 1 on another), the free
       // lanes stay free, the inner loop returns at once and the next refill goes on.
+      // (diagnostic build: before a preparation the stages count as preparation time,
+      // as the r04 / r05 breakdowns did, so that staging is the lookahead's cost)
+      if (prep) IKHIP_DT(kDiagTDrain);  // (scratch slot: the preparation's start)
       bool more = true;
       if (nstage == 0 && (prep || avail <= 24)) { stage1(); more = prep; }
       if (more && nstage == 1 && (prep || avail <= 16)) { stage2(); more = prep; }
       if (more && nstage == 2 && (prep || avail <= 8)) stage3();
-      IKHIP_DT_ACC(kDiagStageTicks, kDiagTSub);
+      if (!prep) IKHIP_DT_ACC(kDiagStageTicks, kDiagTSub);
       if (prep && nstage == 3) {
         IKHIP_DG(kDiagGrabs, 1);
-        IKHIP_DT(kDiagTDrain);  // (scratch slot: the preparation's start)
         // prepare: limits check and seed pose of the batch, one entry per lane
         pcount = ncount;
         nstage = 0;
