@@ -9,10 +9,11 @@
 // Two pipelines (DESIGN.md "FABRIK"):
 //  * fused (default): classify + scatter (the hard-first work order, 6 bytes
 //    per point) -> iter_kernel: persistent; each wave prepares batches of seed
-//    poses in registers, refills a lane whose point converged from them (so a
-//    wave no longer waits for its slowest lane), parks finished lanes in LDS and
-//    runs the angles step + FK round trip + batch stats on them in batches.
-//    Seed poses and final joints never touch HBM.
+//    poses into its LDS batch, refills the lanes whose points converged from it
+//    (so a wave does not wait for its slowest lane), parks finished lanes in an
+//    LDS ring and runs the angles step + FK round trip + batch stats on them in
+//    batches -> fold (the samples into the cost table).  Seed poses and final
+//    joints never touch HBM.
 //  * simple: everything in one kernel, one point per lane, no refill.
 // Per point the state is 4 joints + goal (15 doubles) held in VGPRs.
 #include <atomic>
@@ -636,8 +637,8 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
 // A lane whose point converged is refilled from the wave's batch of prepared
 // points: a wave grabs a.chunk queue positions at once and each lane prepares one
 // of them -- the goal, the limits check and the seed pose (inverse.py:123-130) --
-// into registers (P*), at full SIMD width; a refill then moves prepared points to
-// the free lanes with cross-lane reads (ds_bpermute), with no memory round trip.
+// into the wave's LDS batch, at full SIMD width; a refill then hands entries to
+// the free lanes (LDS reads), with no memory round trip.
 // A finished lane parks its final joints in the wave's LDS ring at the next
 // refill; when the ring would overflow, and at the end, the whole wave runs the
 // angles step on it, one entry per lane (finish_point).  So the seed pose and
