@@ -882,9 +882,8 @@ fabrik_iter_kernel(FabArgs a) {
       }
       IKHIP_DT_ACC(kDiagParkTicks, kDiagTSub);
       IKHIP_DT(kDiagTSub);
-      // the next batch's stages, one per refill while the last 24 entries of this
-      // one are handed out; a stage consumes what the one before loaded (so the
-      // loads are long done), and prepare() runs the stages still missing
+      // the next batch's three stages (called below: one per refill ahead of time,
+      // or back to back just before a preparation)
       auto stage1 = [&]() {
         if (lane == 0) na = atomicAdd(&a.S->heads[head][0], 1ull);
         nstage = 1;
@@ -892,7 +891,7 @@ fabrik_iter_kernel(FabArgs a) {
       auto stage2 = [&]() {
         // the grab's chunk: head h's k-th is the queue's (k * kQueueHeads + h)-th
         // (lane 0's value read into SGPRs: a shuffle would leave the batch's count,
-        // cursor and the hand-out loop divergent in the compiler's eyes)
+        // cursor and the hand-out divergent in the compiler's eyes)
         const uint64_t na0 =
             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(na >> 32), 0) << 32) |
             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)na, 0);
