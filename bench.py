@@ -50,7 +50,6 @@ FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
 HBM_PEAK = 8.0e12           # bytes/s
 FABRIK_FLOP_PER_ITER = 132  # per executed reference iteration
 FABRIK_FLOP_PER_POINT = 150  # + the seed FK and angles, per point
-SPIN_CYCLES = 4_000_000     # the spin ahead of the per-kernel event step (~2 ms at 2.2 GHz)
 
 
 def launch_command(argv, gpus, port):
@@ -653,10 +652,10 @@ def run_fk(job, args):
                        "frac": achieved / HBM_PEAK if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"],
-                       "kernel_ms_note": "events bracket one launch of 1M points queued behind "
-                                         "a device-side spin (dispatch included, the host's "
-                                         "launch latency not); rocprof is the kernel's own "
-                                         "duration",
+                       "kernel_ms_note": "events bracket one launch of 1M points enqueued behind "
+                                         "an untimed one (a 12 us kernel drains before the "
+                                         "host enqueues the next, so the launch latency "
+                                         "stays in); rocprof is the kernel's own duration",
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
                        **prof,
                        "kernel": "fk_kernel", "kernel_ms": k,
@@ -687,13 +686,14 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
     torch.cuda.synchronize()
     if after_warm is not None:
         after_warm()
-    # per-kernel HIP-event durations of one representative step, enqueued behind a
-    # device-side spin (torch's _sleep, on the stream the library shares) so that its
-    # kernels start back to back as in the timed loop: from an idle queue each event
-    # pair also held the host's launch latency (r04 VERDICT: FABRIK's iteration kernel
-    # by events 20 us over its rocprof duration)
+    # per-kernel HIP-event durations of one representative step, enqueued right behind
+    # an untimed one (no wait between them) so that its kernels start back to back and
+    # at the clocks of the timed loop: from an idle queue each event pair also held
+    # the host's launch latency (r04 VERDICT: FABRIK's iteration kernel by events 20 us
+    # over its rocprof duration).  (A device-side spin ahead of the step instead left
+    # the long ANN kernels 1-7 % slower by events than the timed loop's steps, r05.)
     ctx.set_timing(True)
-    torch.cuda._sleep(SPIN_CYCLES)
+    step()
     step()
     ctx.sync()
     kernels = {}
