@@ -1013,7 +1013,13 @@ fabrik_iter_kernel(FabArgs a) {
       }
       dry = nstage < 0 && pptr >= pcount;
       IKHIP_DT_ACC(kDiagRefillTicks, kDiagTRefill);
-      prio_drop();
+      // a dry wave's last lanes are the launch's tail: they iterate at priority 1,
+      // ahead of a SIMD partner that still hands out its batch (r05, three boxes:
+      // iteration kernel -0.7..-1.0 % at tol 1e-3, -0.8..-1.8 % at 1e-5; priority 3,
+      // above the partner's refill and angles steps, and refilling at 4 / 8 free
+      // lanes once the queue is dry both measured slower: profiles/r05/lease_dry/)
+      if (dry) __builtin_amdgcn_s_setprio(1);
+      else prio_drop();
     }
     // iterate until a refill is due (REFILL_MIN lanes free) or, once the queue is
     // dry, until every lane has stopped: the refill's scalar state stays out of

@@ -2,7 +2,8 @@
 bench method over its TIMED window only.
 
 The profiled command is the bench's own (all secondaries, same order, same
-warm-up), so every kernel's dispatches come in blocks of warmup + 1 + steps, one
+warm-up), so every kernel's dispatches come in blocks of warmup + 2 + steps (the
+untimed step and the per-kernel event step between warm-up and timed loop, r05), one
 block per method that launches it, in the bench's method order (ann, fabrik,
 fabrik_tol1e-5, ann_bf16x6, ann_fp16x3, fk); the last `steps` dispatches of a block
 are the timed ones.  Per (method, kernel):
@@ -46,6 +47,11 @@ METHODS_OF = {"ann_fused_kernel": ["ann"],
               "fabrik_iter_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fabrik_fold_kernel": ["fabrik", "fabrik_tol1e-5"],
               "fk_kernel": ["fk"]}
+
+
+# bench.timed(): an untimed step, then the per-kernel event step, between the warm-up
+# and the timed loop
+EVENT_STEPS = 2
 
 
 def _rows(d, pat):
@@ -105,7 +111,7 @@ def main():
             continue
         ids = [i for i, _ in tr[k]]
         ms = dict(tr[k])
-        for m, win in windows(ids, methods, args.warmup + 1 + args.steps, args.steps).items():
+        for m, win in windows(ids, methods, args.warmup + EVENT_STEPS + args.steps, args.steps).items():
             w = [ms[i] for i in win]
             if w:
                 res[m][k] = {"rocprof_avg_ms": sum(w) / len(w), "rocprof_min_ms": min(w),
@@ -118,7 +124,7 @@ def main():
                                             "note": "median over all the run's dispatches"}
     pmc = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
     clocks = defaultdict(lambda: defaultdict(list))
-    pblock = args.warmup + 1 + args.pmc_steps
+    pblock = args.warmup + EVENT_STEPS + args.pmc_steps
     for d in sorted(glob.glob(os.path.join(args.dir, "pmc_*"))):
         if not os.path.isdir(d):
             continue
