@@ -652,10 +652,9 @@ def run_fk(job, args):
                        "frac": achieved / HBM_PEAK if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"],
-                       "kernel_ms_note": "events bracket one launch of 1M points enqueued behind "
-                                         "an untimed one (a 12 us kernel drains before the "
-                                         "host enqueues the next, so the launch latency "
-                                         "stays in); rocprof is the kernel's own duration",
+                       "kernel_ms_note": "events bracket one launch of 1M points (its fixed "
+                                         "launch cost included); rocprof is the kernel's own "
+                                         "duration",
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
                        **prof,
                        "kernel": "fk_kernel", "kernel_ms": k,
@@ -686,14 +685,16 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
     torch.cuda.synchronize()
     if after_warm is not None:
         after_warm()
-    # per-kernel HIP-event durations of one representative step, enqueued right behind
-    # an untimed one (no wait between them) so that its kernels start back to back and
-    # at the clocks of the timed loop: from an idle queue each event pair also held
-    # the host's launch latency (r04 VERDICT: FABRIK's iteration kernel by events 20 us
-    # over its rocprof duration).  (A device-side spin ahead of the step instead left
-    # the long ANN kernels 1-7 % slower by events than the timed loop's steps, r05.)
+    # per-kernel HIP-event durations of one representative step, from an idle queue.
+    # An event's timestamp is taken when the command processor reaches its marker,
+    # which does not wait for the kernels ahead of it on the stream: a kernel that
+    # follows others in the step (FABRIK's iteration kernel after classify and
+    # scatter) is timed with their tail, and any kernel with the host's launch
+    # latency; rocprof's kernel durations (profiles/) are the kernels' own.  (r05:
+    # enqueued behind an untimed step, the events also took in that step's last
+    # kernel -- FK 34 us against 13 by rocprof; behind a device-side spin the long
+    # ANN kernels ran 1-7 % slower than in the timed loop: both dropped.)
     ctx.set_timing(True)
-    step()
     step()
     ctx.sync()
     kernels = {}

@@ -2,8 +2,8 @@
 bench method over its TIMED window only.
 
 The profiled command is the bench's own (all secondaries, same order, same
-warm-up), so every kernel's dispatches come in blocks of warmup + 2 + steps (the
-untimed step and the per-kernel event step between warm-up and timed loop, r05), one
+warm-up), so every kernel's dispatches come in blocks of warmup + E + steps (E: the
+per-kernel event step, 1; the r05 re-entry lease's bench also ran an untimed step, 2), one
 block per method that launches it, in the bench's method order (ann, fabrik,
 fabrik_tol1e-5, ann_bf16x6, ann_fp16x3, fk); the last `steps` dispatches of a block
 are the timed ones.  Per (method, kernel):
@@ -49,9 +49,9 @@ METHODS_OF = {"ann_fused_kernel": ["ann"],
               "fk_kernel": ["fk"]}
 
 
-# bench.timed(): an untimed step, then the per-kernel event step, between the warm-up
-# and the timed loop
-EVENT_STEPS = 2
+# bench.timed(): the per-kernel event step between the warm-up and the timed loop
+# (--event-steps; profiles/r05/lease_f was made by a bench with one more, untimed)
+EVENT_STEPS = 1
 
 
 def _rows(d, pat):
@@ -102,6 +102,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pmc-steps", type=int, default=5)
+    ap.add_argument("--event-steps", type=int, default=EVENT_STEPS)
     ap.add_argument("--out", required=True)
     args = ap.parse_args()
     res = defaultdict(dict)  # method -> kernel -> figures
@@ -111,7 +112,7 @@ def main():
             continue
         ids = [i for i, _ in tr[k]]
         ms = dict(tr[k])
-        for m, win in windows(ids, methods, args.warmup + EVENT_STEPS + args.steps, args.steps).items():
+        for m, win in windows(ids, methods, args.warmup + args.event_steps + args.steps, args.steps).items():
             w = [ms[i] for i in win]
             if w:
                 res[m][k] = {"rocprof_avg_ms": sum(w) / len(w), "rocprof_min_ms": min(w),
@@ -124,7 +125,7 @@ def main():
                                             "note": "median over all the run's dispatches"}
     pmc = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
     clocks = defaultdict(lambda: defaultdict(list))
-    pblock = args.warmup + EVENT_STEPS + args.pmc_steps
+    pblock = args.warmup + args.event_steps + args.pmc_steps
     for d in sorted(glob.glob(os.path.join(args.dir, "pmc_*"))):
         if not os.path.isdir(d):
             continue
