@@ -738,8 +738,8 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 // distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
 // Every solve reaching this kernel runs at least one iteration (the host sends
 // the others to fabrik_simple_kernel), so the seed's last joint is never needed.
-#ifndef IKHIP_FAB_REFILL  // free lanes that trigger a refill (r05: 16 against 6 / 8 / 12 / 20 / 24 / 32)
-#define IKHIP_FAB_REFILL 16
+#ifndef IKHIP_FAB_REFILL  // free lanes that trigger a refill (r05: 12 against 6 / 8 / 16 / 20 / 24 / 32; 12 since the dry waves' raised priority)
+#define IKHIP_FAB_REFILL 12
 #endif
 #ifndef IKHIP_ITER_WAVES
 #define IKHIP_ITER_WAVES 2
