@@ -50,6 +50,7 @@ FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
 HBM_PEAK = 8.0e12           # bytes/s
 FABRIK_FLOP_PER_ITER = 132  # per executed reference iteration
 FABRIK_FLOP_PER_POINT = 150  # + the seed FK and angles, per point
+TIMING_REPS = 5             # single steps timed per kernel (median)
 
 
 def launch_command(argv, gpus, port):
@@ -231,12 +232,23 @@ def profile_fields(path, kernel):
     return out
 
 
-def roofline_fracs(work, kernel_ms, peak, prof):
+def kernel_time_ok(kernel_ms, step_ms):
+    """A kernel's measured duration can be a roofline's denominator only if it
+    fits inside the step that launches it (a begin marker that
+    took in the kernels ahead of it gave an iteration kernel longer than its
+    whole step)."""
+    return bool(kernel_ms) and bool(step_ms) and kernel_ms <= step_ms
+
+
+def roofline_fracs(work, kernel_ms, peak, prof, step_ms=None):
     """The roofline's achieved rate both ways: from this run's
-    HIP-event kernel time and from the committed rocprof window average of the
-    same kernel (`prof`: profile_fields); `frac` / `achieved` headline the
-    LOWER of the two.  work: algorithmic flop (or bytes) per launch."""
-    ev = work / (kernel_ms / 1e3) if kernel_ms else None
+    HIP-event kernel time (the dispatch's own start / end stamps) and from the
+    committed rocprof window average of the same kernel (`prof`:
+    profile_fields); `frac` / `achieved` headline the LOWER of the two.  An
+    events duration longer than the step (`step_ms`, kernel_time_ok) is not a
+    kernel duration and is dropped.  work: algorithmic flop (or bytes) per launch."""
+    valid = kernel_time_ok(kernel_ms, step_ms) if step_ms is not None else bool(kernel_ms)
+    ev = work / (kernel_ms / 1e3) if valid else None
     rp = prof.get("rocprof_avg_ms")
     rq = work / (rp / 1e3) if rp else None
     cands = [x for x in (ev, rq) if x]
@@ -244,7 +256,7 @@ def roofline_fracs(work, kernel_ms, peak, prof):
     return {"achieved_events": ev, "frac_events": ev / peak if ev else None,
             "achieved_rocprof": rq, "frac_rocprof": rq / peak if rq else None,
             "headline": None if head is None else ("rocprof" if head == rq else "events"),
-            "_head": head}
+            "kernel_ms_valid": valid, "_head": head}
 
 
 def load_pipe(path, kernel):
@@ -474,13 +486,13 @@ def run_ann(job, args, mode="fp32"):
             (BF16_MFMA_PEAK if mode == "bf16x6" else FP16_MFMA_PEAK) / SPLIT_PRODUCTS[mode])
     traffic = load_traffic(args.traffic_file, kname)
     prof = profile_fields(args.traffic_file, kname)
-    fr = roofline_fracs(flop_pt * n, k, peak, prof)
+    fr = roofline_fracs(flop_pt * n, k, peak, prof, res["ms_per_step"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
                        "peak": peak / 1e12, "unit": "TFLOP/s",
                        "frac": achieved / peak if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
-                       "frac_headline": fr["headline"],
+                       "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
                        "traffic": traffic, "kernel": kname,
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
                        "points_per_launch": n, **prof}
@@ -596,13 +608,13 @@ def run_fabrik(job, args, tol=None, max_iter=None):
         "fabrik_tol1e-5/fabrik_iter_kernel"
     traffic = load_traffic(args.traffic_file, pkey)
     prof = profile_fields(args.traffic_file, pkey)
-    fr = roofline_fracs(flops, k, FP64_VALU_PEAK, prof)
+    fr = roofline_fracs(flops, k, FP64_VALU_PEAK, prof, res["ms_per_step"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "valu_fp64", "achieved": achieved / 1e12 if achieved else None,
                        "peak": FP64_VALU_PEAK / 1e12, "unit": "TFLOP/s",
                        "frac": achieved / FP64_VALU_PEAK if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
-                       "frac_headline": fr["headline"],
+                       "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
                        "algorithmic_flop_per_point": FABRIK_FLOP_PER_POINT,
@@ -645,13 +657,13 @@ def run_fk(job, args):
     res["outputs"] = {"xyz": dxyz}
     k = res["kernels"].get("fk_kernel")
     prof = profile_fields(args.traffic_file, "fk_kernel")
-    fr = roofline_fracs(FK_BYTES_PER_POINT * n, k, HBM_PEAK, prof)
+    fr = roofline_fracs(FK_BYTES_PER_POINT * n, k, HBM_PEAK, prof, res["ms_per_step"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None,
                        "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                        "frac": achieved / HBM_PEAK if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
-                       "frac_headline": fr["headline"],
+                       "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
                        "kernel_ms_note": "events bracket one launch of 1M points (its fixed "
                                          "launch cost included); rocprof is the kernel's own "
                                          "duration",
@@ -685,21 +697,22 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
     torch.cuda.synchronize()
     if after_warm is not None:
         after_warm()
-    # per-kernel HIP-event durations of one representative step, from an idle queue.
-    # An event's timestamp is taken when the command processor reaches its marker,
-    # which does not wait for the kernels ahead of it on the stream: a kernel that
-    # follows others in the step (FABRIK's iteration kernel after classify and
-    # scatter) is timed with their tail, and any kernel with the host's launch
-    # latency; rocprof's kernel durations (profiles/) are the kernels' own.  (r05:
-    # enqueued behind an untimed step, the events also took in that step's last
-    # kernel -- FK 34 us against 13 by rocprof; behind a device-side spin the long
-    # ANN kernels ran 1-7 % slower than in the timed loop: both dropped.)
+    # per-kernel durations: the library launches each kernel of a timed call with
+    # hipExtLaunchKernel's start / stop events, which the dispatch itself stamps
+    # (ik_ctx_set_timing), so a kernel's interval holds neither the
+    # kernels ahead of it in the step nor the host's launch latency.  Median of
+    # TIMING_REPS single steps, each from an idle queue.
     ctx.set_timing(True)
-    step()
-    ctx.sync()
-    kernels = {}
-    for name, ms in ctx.kernel_times():
-        kernels[name] = kernels.get(name, 0.0) + ms
+    per = {}
+    for _ in range(TIMING_REPS):
+        step()
+        ctx.sync()
+        one = {}
+        for name, ms in ctx.kernel_times():
+            one[name] = one.get(name, 0.0) + ms
+        for name, ms in one.items():
+            per.setdefault(name, []).append(ms)
+    kernels = {name: float(np.median(v)) for name, v in per.items()}
     ctx.set_timing(False)
     torch.cuda.synchronize()
     barrier(world)
@@ -972,6 +985,57 @@ def secondary_entry(key, r2, total, world, args):
     if cref:
         e["baseline_config"] = cref
     return e
+
+
+DRIVER_TIMEOUT_S = 600  # the driver's limit on one bench.py run (BENCH_r05.json timeout_s)
+# measured per-step times at 1M points per rank (profiles/r05/lease_bench_default.json)
+LEG_STEP_MS = {"ann": 39.2, "fabrik": 0.36, "fabrik_tol1e-5": 0.51, "ann_bf16x6": 21.9,
+               "ann_fp16x3": 12.7, "fk": 0.023}
+E2E_BYTES_PER_POINT = {"ann": 24 + 16, "fabrik": 24 + 32}
+PCIE_BYTES_PER_S = 50e9   # tools/pcie_probe.py: ~55 GB/s, the directions do not overlap
+STARTUP_S = 120.0         # first `import torch` + HIP init on a fresh box (1-2 min)
+RCCL_INIT_S = 30.0        # communicator setup on the success path (bounded by the deadline)
+BATCH_GEN_S_PER_M = 0.2   # random_dist, seconds per million points (1.4 s for 10M here)
+
+
+def wall_budget(world, steps, warmup, rccl_timeout_s=120.0, points=1_000_000, cpu_seconds=10.0):
+    """An upper estimate of one `bench.py --gpus N` run's wall time, in seconds,
+    by leg (the driver's first N = 8 run must fit its 600 s
+    limit).  Each leg: W warm-up + TIMING_REPS event-timed + K timed steps, the
+    untimed gather check (N > 1: two parts re-solved), 20 end-to-end calls each
+    way (pinned / pageable, the whole batch through PCIe), and its batch
+    generation; plus start-up, RCCL init and, at N > 1, the two strong legs on
+    10M points.  `stall_path_s`: the longest a run whose collective never
+    completes can last before IKHIP_RCCL_TIMEOUT_S aborts it."""
+    total = points * world
+    per_rank_m = points / 1e6
+    legs = {}
+    for key, ms in LEG_STEP_MS.items():
+        n_steps = warmup + TIMING_REPS + steps + (2 if world > 1 else 0)
+        t = n_steps * ms * per_rank_m / 1e3
+        method = "fabrik" if key.startswith("fabrik") else ("ann" if key.startswith("ann") else None)
+        if method:
+            e2e = (ms * per_rank_m / 1e3 + total * E2E_BYTES_PER_POINT[method] / PCIE_BYTES_PER_S)
+            t += 2 * 20 * e2e
+        if method == "fabrik":
+            t += BATCH_GEN_S_PER_M * total / 1e6 + 6 * ms * per_rank_m / 1e3  # warm batch + cold
+        legs[key] = t
+    if world > 1:
+        sm = STRONG_POINTS / world / 1e6
+        for key, base in (("ann_strong10M", "ann"), ("fabrik_tol1e-5_strong10M", "fabrik_tol1e-5")):
+            n_steps = warmup + TIMING_REPS + steps + 2
+            legs[key] = (n_steps * LEG_STEP_MS[base] * sm / 1e3
+                         + BATCH_GEN_S_PER_M * STRONG_POINTS / 1e6
+                         + (BATCH_GEN_S_PER_M * STRONG_POINTS / 1e6 if base.startswith("fabrik")
+                            else 0.0))
+    fixed = {"startup": STARTUP_S, "rccl_init": RCCL_INIT_S if world > 1 else 0.0,
+             "batch": BATCH_GEN_S_PER_M * total / 1e6, "model_loads": 4 * 2.0,
+             # rank 0 at N = 1: the ANN and FABRIK oracles, cpu_seconds each (+ one pass)
+             "cpu_baseline": 2 * (cpu_seconds + 2.0) if world == 1 else 0.0}
+    total_s = sum(legs.values()) + sum(fixed.values())
+    return {"legs_s": legs, "fixed_s": fixed, "total_s": total_s,
+            "stall_path_s": total_s + rccl_timeout_s,
+            "limit_s": DRIVER_TIMEOUT_S}
 
 
 def strong_job(ctx, sc, world, rank, total):

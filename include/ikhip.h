@@ -189,9 +189,18 @@ int ik_ann_solve(ik_ctx *ctx, const double *pts, int64_t n, float *ang, double *
 enum { IK_ANN_FP32 = 0, IK_ANN_BF16X6 = 1, IK_ANN_FP16X3 = 2 };
 int ik_ann_set_mode(ik_ctx *ctx, int mode);
 int ik_ann_get_mode(ik_ctx *ctx); /* the mode, or -ik_status */
+/* The arithmetic the next ik_ann_solve runs for the loaded model (or
+ * -ik_status; -IK_E_NOMODEL before ik_ann_load): the set mode, or IK_ANN_FP32
+ * when no layer of the model can take it (a fused model wider than 512, or the
+ * split planes left out at load because only the fp32 operands fit the
+ * device), or IK_ANN_BF16X6 for IK_ANN_FP16X3 on the layered path. */
+int ik_ann_effective_mode(ik_ctx *ctx);
 
-/* Per-kernel timing with HIP events on the context's stream: when on, every
- * kernel a call launches is bracketed by hipEventRecord.  ik_kernel_times
+/* Per-kernel timing with HIP events: when on, every kernel a call launches
+ * goes through hipExtLaunchKernel with a start and a stop event, which the
+ * dispatch itself stamps (the kernel's own start and end: not the kernels ahead
+ * of it on the stream, not the host's launch latency); the RCCL gather of a
+ * sharded call is bracketed by stream markers.  ik_kernel_times
  * waits for the last call's events and returns how many kernels it timed,
  * their durations in ms and (if names != NULL) their names, name_len bytes
  * each; a negative value is -ik_status. */
@@ -302,9 +311,10 @@ int ik_comm_destroy(ik_ctx *ctx);
  * count the last sharded call was planned with (ik_shard_plan_of's chunks; 0
  * before one), so a caller can find its own rows with ik_shard_part. */
 int ik_comm_info(ik_ctx *ctx, int *nranks, int *rank, int *last_chunks);
-/* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic: ANN 1
- * (one in-place all-gather after the solve), FABRIK 2 when nranks > 1 (chunk 0's
- * gather under chunk 1's solve).  Every rank must use the same value:
+/* Chunks per sharded call (1..IK_MAX_GATHER_CHUNKS), or 0 = automatic: one
+ * chunk for both methods (one in-place all-gather after the solve; C >= 2
+ * overlaps chunk c's gather with chunk c + 1's solve, opt-in until a real
+ * N >= 2 run has bit-checked it).  Every rank must use the same value:
  * each call's tail carries its plan (n, chunks, method) and a rank whose plan
  * differs from rank 0's fails the call with IK_E_RCCL.  Environment default:
  * IKHIP_GATHER_CHUNKS (checked equal on every rank by ik_comm_init). */

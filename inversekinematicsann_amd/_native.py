@@ -35,6 +35,7 @@ EXPORTED_SYMBOLS = ("ik_ctx_create", "ik_ctx_destroy", "ik_ctx_set_stream", "ik_
                     "ik_fabrik_solve", "ik_fabrik_solve_fk", "ik_fabrik_calc", "ik_fabrik_reset_order", "ik_ann_load", "ik_ann_solve",
                     "ik_stats_fetch", "ik_ctx_set_timing", "ik_kernel_times",
                     "ik_ctx_set_debug", "ik_debug_read", "ik_ann_set_mode", "ik_ann_get_mode",
+                    "ik_ann_effective_mode",
                     "ik_comm_unique_id", "ik_comm_init", "ik_comm_init_loopback",
                     "ik_loopback_byte", "ik_comm_destroy", "ik_comm_info",
                     "ik_comm_set_chunks", "ik_shard_plan_of", "ik_shard_part", "ik_shard_range",
@@ -138,6 +139,7 @@ def load_library(path: str = LIB_PATH):
         L.ik_debug_read.argtypes = [vp, vp, ctypes.c_int]
         L.ik_ann_set_mode.argtypes = [vp, ctypes.c_int]
         L.ik_ann_get_mode.argtypes = [vp]
+        L.ik_ann_effective_mode.argtypes = [vp]
         L.ik_host_alloc.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]
         L.ik_host_free.argtypes = [vp]
         L.ik_comm_unique_id.argtypes = [vp]
@@ -414,12 +416,37 @@ class Context:
         sc = [_host(v, np.float64).reshape(-1) for v in (x_mean, x_scale, y_mean, y_scale)]
         self._check(self.lib.ik_ann_load(self.handle, nl, _ptr(dims_a), _ptr(acts_a), wp, bp,
                                          *[_ptr(v) for v in sc]))
+        self._warn_mode()
 
     def ann_set_mode(self, mode: str):
         """Hidden-layer GEMM arithmetic: "fp32" (default), "bf16x6" or "fp16x3" (ikhip.h)."""
         if mode not in ANN_MODES:
             raise ValueError(f"unknown ANN mode {mode!r}; expected one of {sorted(ANN_MODES)}")
         self._check(self.lib.ik_ann_set_mode(self.handle, ANN_MODES[mode]))
+        self._warn_mode()
+
+    def ann_effective_mode(self) -> str:
+        """The arithmetic the next ANN solve runs for the loaded model
+        (ik_ann_effective_mode): the set mode, or "fp32" when no layer can take it
+        (a fused model wider than 512, or split planes left out at load because
+        the device had room only for the fp32 operands), or "bf16x6" for
+        "fp16x3" on the layered path."""
+        m = self.lib.ik_ann_effective_mode(self.handle)
+        if m < 0:
+            raise NativeError(-m, self.lib.ik_last_error().decode())
+        return {v: k for k, v in ANN_MODES.items()}[m]
+
+    def _warn_mode(self):
+        """Say so when a loaded model runs another arithmetic than the set mode."""
+        want = self.ann_mode()
+        if want == "fp32" or self.lib.ik_ann_effective_mode(self.handle) < 0:
+            return
+        got = self.ann_effective_mode()
+        if got != want:
+            import warnings
+            warnings.warn(f"ANN mode {want!r} is not available for the loaded model; its "
+                          f"solves run {got!r} (ik_ann_effective_mode)", RuntimeWarning,
+                          stacklevel=3)
 
     def ann_mode(self) -> str:
         m = self.lib.ik_ann_get_mode(self.handle)

@@ -1077,7 +1077,7 @@ void launch_ann_wide(const AnnModelDev &m, const RobotDev &r, const double *pts,
   const int64_t ntiles = (n + 31) / 32;
   const unsigned grid = (unsigned)(ntiles < cus ? ntiles : cus);
   kt_begin("ann_fused_kernel_wide", st);
-  hipLaunchKernelGGL((ann_fused_kernel<1, 0>), dim3(grid), dim3(256), 0, st, a);
+  IK_LAUNCH((ann_fused_kernel<1, 0>), dim3(grid), dim3(256), 0, st, a);
   kt_end(st);
 }
 
@@ -1259,10 +1259,10 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
   if (xmode)
     launch_ann_kernel_x(mr, xmode, grid, st, a);
   else if (mr == 2)
-    hipLaunchKernelGGL((ann_fused_kernel<2, 0>), dim3(grid), dim3(64 * ann_waves<2, 0>()), 0, st,
+    IK_LAUNCH((ann_fused_kernel<2, 0>), dim3(grid), dim3(64 * ann_waves<2, 0>()), 0, st,
                        a);
   else
-    hipLaunchKernelGGL((ann_fused_kernel<1, 0>), dim3(grid), dim3(256), 0, st, a);
+    IK_LAUNCH((ann_fused_kernel<1, 0>), dim3(grid), dim3(256), 0, st, a);
   kt_end(st);
 }
 
@@ -1271,7 +1271,7 @@ void launch_ann(const AnnModelDev &m, const RobotDev &r, const double *pts, int6
 void ann::launch_ann_kernel_x(int mr, int xmode, unsigned grid, hipStream_t st,
                               const AnnArgs &a) {
 #define IK_X(M, X) \
-  hipLaunchKernelGGL((ann_fused_kernel<M, X>), dim3(grid), dim3(64 * ann_waves<M, X>()), 0, st, a)
+  IK_LAUNCH((ann_fused_kernel<M, X>), dim3(grid), dim3(64 * ann_waves<M, X>()), 0, st, a)
   if (mr == 2) {
     if (xmode == 2) IK_X(2, 2); else IK_X(2, 1);
   } else {

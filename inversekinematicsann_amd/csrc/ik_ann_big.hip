@@ -593,7 +593,7 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
     const int64_t rows = (n - p0) < chunk_rows ? (n - p0) : chunk_rows;
     const unsigned g1 = (unsigned)((rows + 255) / 256);
     kt_begin("annb_in_kernel", st);
-    hipLaunchKernelGGL(annb_in_kernel, dim3(g1), dim3(256), 0, st, pts, p0, rows, m.xm[0],
+    IK_LAUNCH(annb_in_kernel, dim3(g1), dim3(256), 0, st, pts, p0, rows, m.xm[0],
                        m.xm[1], m.xm[2], m.xs[0], m.xs[1], m.xs[2], r, check_limits ? 1 : 0,
                        buf[0], S);
     kt_end(st);
@@ -613,7 +613,7 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
         const int64_t xgroups = (xRB + BH - 1) / BH * ((nCB + BW - 1) / BW);
         const dim3 xgrid((unsigned)((xgroups + 7) / 8 * 8 * BH * BW));
         kt_begin("annb_gemm_x6_kernel", st);
-        hipLaunchKernelGGL(annb_gemm_x6_kernel, xgrid, dim3(512), 0, st, buf[cur], lda, rows,
+        IK_LAUNCH(annb_gemm_x6_kernel, xgrid, dim3(512), 0, st, buf[cur], lda, rows,
                            L.wx, lda / 32, L.np, L.bias, L.act, buf[cur ^ 1], L.np);
         kt_end(st);
         cur ^= 1;
@@ -622,11 +622,11 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
       }
       kt_begin("annb_gemm_kernel", st);
       if (NT == 1)
-        hipLaunchKernelGGL(annb_gemm_kernel<1>, grid, dim3(256), 0, st, buf[cur], lda, rows,
+        IK_LAUNCH(annb_gemm_kernel<1>, grid, dim3(256), 0, st, buf[cur], lda, rows,
                            reinterpret_cast<const f32x4 *>(L.wp), G, NT, L.bias, L.act,
                            buf[cur ^ 1], L.np);
       else
-        hipLaunchKernelGGL(annb_gemm_kernel<2>, grid, dim3(256), 0, st, buf[cur], lda, rows,
+        IK_LAUNCH(annb_gemm_kernel<2>, grid, dim3(256), 0, st, buf[cur], lda, rows,
                            reinterpret_cast<const f32x4 *>(L.wp), G, NT, L.bias, L.act,
                            buf[cur ^ 1], L.np);
       kt_end(st);
@@ -634,7 +634,7 @@ void launch_ann_big(const AnnBigModel &m, const RobotDev &r, const double *pts, 
       lda = L.np;
     }
     kt_begin("annb_out_kernel", st);
-    hipLaunchKernelGGL(annb_out_kernel, dim3(g1), dim3(256), 0, st, buf[cur], lda, pts, p0, rows,
+    IK_LAUNCH(annb_out_kernel, dim3(g1), dim3(256), 0, st, buf[cur], lda, pts, p0, rows,
                        o, ang, fk_err, S);
     kt_end(st);
   }

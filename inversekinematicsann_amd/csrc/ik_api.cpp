@@ -79,15 +79,30 @@ int seed_order(ik_ctx *c, double tol, int max_iter) {
 }  // namespace ikapi
 
 namespace ikhip {
-void kt_begin(const char *name, hipStream_t st) {
+void kt_begin(const char *name, hipStream_t) {
   if (!g_kt || !g_kt->on || g_kt->n >= kMaxTimed) return;
   g_kt->name[g_kt->n] = name;
+  g_kt->state = 1;
+}
+void kt_span_begin(const char *name, hipStream_t st) {
+  if (!g_kt || !g_kt->on || g_kt->n >= kMaxTimed) return;
+  g_kt->name[g_kt->n] = name;
+  g_kt->state = 3;
   (void)hipEventRecord(g_kt->beg[g_kt->n], st);
+}
+bool kt_take_events(hipEvent_t *beg, hipEvent_t *end) {
+  if (!g_kt || !g_kt->on || g_kt->n >= kMaxTimed || g_kt->state != 1) return false;
+  *beg = g_kt->beg[g_kt->n];
+  *end = g_kt->end[g_kt->n];
+  g_kt->state = 2;
+  return true;
 }
 void kt_end(hipStream_t st) {
   if (!g_kt || !g_kt->on || g_kt->n >= kMaxTimed) return;
-  (void)hipEventRecord(g_kt->end[g_kt->n], st);
-  g_kt->n++;
+  if (g_kt->state == 3) (void)hipEventRecord(g_kt->end[g_kt->n], st);
+  // a slot armed without a stamped launch (no kernel ran) is dropped
+  if (g_kt->state == 2 || g_kt->state == 3) g_kt->n++;
+  g_kt->state = 0;
 }
 }  // namespace ikhip
 
@@ -101,6 +116,7 @@ int fail(int code, const std::string &msg) {
 KtScope::KtScope(ik_ctx *c) : c_(c) {
   g_kt = &c->kt;
   c->kt.n = 0;
+  c->kt.state = 0;
   // calls on one context share its stats block and work-queue words: a call on
   // another stream than the last one starts after that one's work
   if (c->call_done_set && c->last_stream && c->last_stream != c->stream)
@@ -205,15 +221,28 @@ int ann_launch(ik_ctx *c, const double *dp, int64_t n, float *da, double *de, bo
     if (rows < 128) rows = 128;
     const int64_t n128 = (n + 127) / 128 * 128;
     if (rows > n128) rows = n128;
-    const size_t bytes = 2 * (size_t)rows * ld * sizeof(float);
-    if (bytes > c->ann_act_bytes) {
+    if (2 * (size_t)rows * ld * sizeof(float) > c->ann_act_bytes) {
       IK_HIP(hipStreamSynchronize(c->stream));
       if (c->ann_act) IK_HIP(hipFree(c->ann_act));
       c->ann_act = nullptr;
       c->ann_act_bytes = 0;
-      IK_HIP(hipMalloc(&c->ann_act, bytes));
-      c->ann_act_bytes = bytes;
+      // the budget's rows, or fewer (down to one 128-row tile, which ik_ann_load
+      // checked would fit) when the device has less free
+      for (;;) {
+        const size_t bytes = 2 * (size_t)rows * ld * sizeof(float);
+        const hipError_t e = hipMalloc(&c->ann_act, bytes);
+        if (e == hipSuccess) {
+          c->ann_act_bytes = bytes;
+          break;
+        }
+        (void)hipGetLastError();
+        if (e != hipErrorOutOfMemory || rows <= 128) IK_HIP(e);
+        rows = (rows / 2 + 127) / 128 * 128;
+      }
     }
+    // the rows the buffers hold (a smaller earlier allocation limits the chunk)
+    const int64_t fit = (int64_t)(c->ann_act_bytes / (2 * ld * sizeof(float))) / 128 * 128;
+    if (rows > fit) rows = fit;
     // (both split modes run bf16x6 here: fp16x3's bounded-input planes are the
     // fused kernel's)
     launch_ann_big(c->ann_bigm, c->robot, dp, n, da, de, limits, S, c->stream,
@@ -377,6 +406,7 @@ int ik_ctx_set_timing(ik_ctx *c, int on) {
   }
   c->kt.on = on != 0;
   c->kt.n = 0;
+  c->kt.state = 0;
   return IK_OK;
 }
 
@@ -778,14 +808,30 @@ int ik_ann_load(ik_ctx *c, int n_layers, const int32_t *dims, const int32_t *act
   c->ann_loaded = false;
   size_t dev_free = 0, dev_total = 0;
   IK_HIP(hipMemGetInfo(&dev_free, &dev_total));
-  if (total > dev_free) {  // without the split planes (the split modes then run fp32)?
+  // the layered path's first solve also needs its two activation buffers: at
+  // least one 128-row tile of the widest padded layer (ann_launch takes up to
+  // IKHIP_ANN_ACT_MB and falls back to fewer rows when that much is not free;
+  // ADVICE r05), less what a previous model's buffers already hold
+  size_t act_min = 0;
+  if (big) {
+    size_t ld = 8;
+    for (int l = 0; l < n_layers; ++l) {
+      const size_t np = (size_t)(dims[l + 1] + 31) / 32 * 32;
+      ld = np > ld ? np : ld;
+    }
+    act_min = 2 * 128 * ld * sizeof(float);
+    act_min = act_min > c->ann_act_bytes ? act_min - c->ann_act_bytes : 0;
+  }
+  if (total + act_min > dev_free) {  // without the split planes (the split modes then run fp32)?
     planes = false;
     layout();
   }
-  if (total > dev_free)
+  if (total + act_min > dev_free)
     return fail(IK_E_HIP, "ik_ann_load: the packed model needs " + std::to_string(total) +
-                              " bytes of device memory, " + std::to_string(dev_free) +
+                              " bytes of device memory (+ " + std::to_string(act_min) +
+                              " for its activations), " + std::to_string(dev_free) +
                               " are free");
+  // (without the planes a split mode runs fp32: ik_ann_effective_mode says so)
   IK_HIP(hipMalloc(&c->ann_buf, total));
   char *base = static_cast<char *>(c->ann_buf);
   // pack and upload one layer's section at a time: the host holds
@@ -870,6 +916,21 @@ int ik_ann_set_mode(ik_ctx *c, int mode) {
 }
 
 int ik_ann_get_mode(ik_ctx *c) { return c ? c->ann_mode : -IK_E_BADARG; }
+
+int ik_ann_effective_mode(ik_ctx *c) {
+  if (!c) return -IK_E_BADARG;
+  if (!c->ann_loaded) return -fail(IK_E_NOMODEL, "ik_ann_effective_mode: no model loaded");
+  if (c->ann_mode == IK_ANN_FP32) return IK_ANN_FP32;
+  if (c->ann_big) {  // both split modes run bf16x6 there
+    for (const AnnBigLayer &L : c->ann_bigm.layers)
+      if (L.wx) return IK_ANN_BF16X6;
+    return IK_ANN_FP32;
+  }
+  const void *const *ops = c->ann_mode == IK_ANN_BF16X6 ? c->ann_wx : c->ann_wh;
+  for (int l = 0; l < c->ann.n_layers; ++l)
+    if (ops[l]) return c->ann_mode;
+  return IK_ANN_FP32;
+}
 
 int ik_ann_solve(ik_ctx *c, const double *pts, int64_t n, float *ang, double *fk_err,
                  int flags, ik_stats *stats) {

@@ -496,9 +496,27 @@ inline void fk_trip_consts(const RobotDev &r, double jc[16], int *alpha_bad) {
 }
 
 // Optional per-kernel HIP-event timing of the current call (ik_ctx_set_timing):
-// launchers bracket every kernel with kt_begin / kt_end.
+// launchers bracket every kernel with kt_begin / IK_LAUNCH / kt_end.  The kernel's
+// events are handed to hipExtLaunchKernel, so the dispatch itself stamps its own
+// start and end: neither the kernels ahead of it on the stream nor the host's
+// launch latency fall inside the interval.  Spans that are not
+// one kernel (the RCCL gather) use kt_span_begin: stream markers.
 void kt_begin(const char *name, hipStream_t st);
+void kt_span_begin(const char *name, hipStream_t st);
 void kt_end(hipStream_t st);
+// the armed slot's events for the kernel about to launch (false: timing is off)
+bool kt_take_events(hipEvent_t *beg, hipEvent_t *end);
+}  // namespace ikhip
+#include <hip/hip_ext.h>
+namespace ikhip {
+#define IK_LAUNCH(K, G, B, SH, ST, ...)                                             \
+  do {                                                                              \
+    hipEvent_t ik_kb_ = nullptr, ik_ke_ = nullptr;                                  \
+    if (::ikhip::kt_take_events(&ik_kb_, &ik_ke_))                                  \
+      hipExtLaunchKernelGGL(K, G, B, SH, ST, ik_kb_, ik_ke_, 0u, __VA_ARGS__);      \
+    else                                                                            \
+      hipLaunchKernelGGL(K, G, B, SH, ST, __VA_ARGS__);                             \
+  } while (0)
 
 void launch_reset_stats(DevStats *S, hipStream_t st);
 void launch_check_limits(const RobotDev &r, const double *pts, int64_t n, DevStats *S,

@@ -266,7 +266,7 @@ __global__ void robot_const_kernel(RobotDev r, FkTrip t, RobotConstDev *rc) {
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t stream) {
   FkTrip t;
   fk_trip_consts(r, t.jc, &t.alpha_bad);
-  hipLaunchKernelGGL(robot_const_kernel, dim3(1), dim3(64), 0, stream, r, t, rc);
+  IK_LAUNCH(robot_const_kernel, dim3(1), dim3(64), 0, stream, r, t, rc);
 }
 
 __device__ __forceinline__ void store_joints(double *dst, int64_t i, const d3 J[4]) {
@@ -1166,13 +1166,13 @@ static int num_cus() {
 template <int REFILL_MIN, bool ORD>
 static void launch_iter(int core, unsigned grid, hipStream_t stream, const FabArgs &a) {
   if (core == 2)
-    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, 2>), dim3(grid), dim3(256), 0,
+    IK_LAUNCH((fabrik_iter_kernel<REFILL_MIN, ORD, 2>), dim3(grid), dim3(256), 0,
                        stream, a);
   else if (core == 1)
-    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, 1>), dim3(grid), dim3(256), 0,
+    IK_LAUNCH((fabrik_iter_kernel<REFILL_MIN, ORD, 1>), dim3(grid), dim3(256), 0,
                        stream, a);
   else
-    hipLaunchKernelGGL((fabrik_iter_kernel<REFILL_MIN, ORD, 0>), dim3(grid), dim3(256), 0,
+    IK_LAUNCH((fabrik_iter_kernel<REFILL_MIN, ORD, 0>), dim3(grid), dim3(256), 0,
                        stream, a);
 }
 
@@ -1219,7 +1219,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   // no iteration at all when the loop's initial errors of 1.0 already pass
   if (variant == 0 || max_iter <= 0 || !(1.0 > a.tol2) || !robot_ok) {
     kt_begin("fabrik_simple_kernel", stream);
-    hipLaunchKernelGGL(fabrik_simple_kernel, dim3(grid), dim3(256), 0, stream, a);
+    IK_LAUNCH(fabrik_simple_kernel, dim3(grid), dim3(256), 0, stream, a);
     kt_end(stream);
     return;
   }
@@ -1232,10 +1232,10 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     p += up256((size_t)n * 4);
     a.cell = reinterpret_cast<uint16_t *>(p);
     kt_begin("fabrik_classify_kernel", stream);
-    hipLaunchKernelGGL(fabrik_classify_kernel, dim3(ogrid), dim3(256), 0, stream, a);
+    IK_LAUNCH(fabrik_classify_kernel, dim3(ogrid), dim3(256), 0, stream, a);
     kt_end(stream);
     kt_begin("fabrik_scatter_kernel", stream);
-    hipLaunchKernelGGL(fabrik_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
+    IK_LAUNCH(fabrik_scatter_kernel, dim3(ogrid), dim3(256), 0, stream, a);
     kt_end(stream);
   }
   // persistent grid: blocks_per_cu 256-thread blocks per CU (= waves per SIMD)
@@ -1278,7 +1278,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   kt_end(stream);
   if (ordered) {
     kt_begin("fabrik_fold_kernel", stream);
-    hipLaunchKernelGGL(fabrik_fold_kernel, dim3(1), dim3(256), 0, stream, a);
+    IK_LAUNCH(fabrik_fold_kernel, dim3(1), dim3(256), 0, stream, a);
     kt_end(stream);
   }
 }
@@ -1393,7 +1393,7 @@ void launch_fabrik_calc(int nj, const double *dists, const double *init, bool in
   const double tol2 = tol_threshold(tol);
 #define IK_CALC_CASE(K)                                                                      \
   case K:                                                                                    \
-    hipLaunchKernelGGL(fabrik_calc_kernel<K>, dim3(grid), dim3(256), 0, st, dists, init, sh, \
+    IK_LAUNCH(fabrik_calc_kernel<K>, dim3(grid), dim3(256), 0, st, dists, init, sh, \
                        goals, n, tol2, max_iter, joints, iters, S);                          \
     break;
   kt_begin("fabrik_calc_kernel", st);
@@ -1406,7 +1406,7 @@ void launch_fabrik_calc(int nj, const double *dists, const double *init, bool in
     IK_CALC_CASE(7)
     IK_CALC_CASE(8)
     default:
-      hipLaunchKernelGGL(fabrik_calc_any_kernel, dim3(grid), dim3(256), 0, st, nj, dists, init,
+      IK_LAUNCH(fabrik_calc_any_kernel, dim3(grid), dim3(256), 0, st, nj, dists, init,
                          sh, goals, n, tol2, max_iter, joints, iters, S);
       break;
   }

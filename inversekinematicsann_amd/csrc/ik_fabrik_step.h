@@ -128,8 +128,12 @@ struct ErrBand {
 };
 
 __host__ __forceinline__ ErrBand fabrik_band(double tol2, double n1max, double sum_l) {
-  ErrBand b = {-1.0, 0.0};
-  if (!(tol2 > 0.0)) return b;  // (hi = 0, lo = -1: every positive error exact)
+  // tol2 <= 0 (tol = 0, or a negative tol): a band that decides nothing, every
+  // comparison exact.  (hi = 0 would call any sea > 0 "above", but at tol = 0 the
+  // reference stops where b0 rounds onto start exactly, se2 == 0, while q is
+  // 1 +- 1 ulp and sea > 0: ADVICE r05.)
+  ErrBand b = {-1.0, INFINITY};
+  if (!(tol2 > 0.0)) return b;
   const double T = std::sqrt(tol2);
   const double tol_lo = T * (1.0 - 0x1p-50), tol_hi = T * (1.0 + 0x1p-50);
   const double d = 0x1p-52 * (3.0 * n1max + 4.0 * sum_l + 1.0);

@@ -31,7 +31,7 @@ __global__ void reset_stats_kernel(DevStats *S) {
 }
 
 void launch_reset_stats(DevStats *S, hipStream_t st) {
-  hipLaunchKernelGGL(reset_stats_kernel, dim3(1), dim3(64), 0, st, S);
+  IK_LAUNCH(reset_stats_kernel, dim3(1), dim3(64), 0, st, S);
 }
 
 // kinematics/inverse.py:26-35 InverseKinematics.check_limits
@@ -48,7 +48,7 @@ void launch_check_limits(const RobotDev &r, const double *pts, int64_t n, DevSta
   if (n <= 0) return;
   unsigned grid = (unsigned)((n + 255) / 256);
   kt_begin("check_limits_kernel", st);
-  hipLaunchKernelGGL(check_limits_kernel, dim3(grid), dim3(256), 0, st, r, pts, n, S);
+  IK_LAUNCH(check_limits_kernel, dim3(grid), dim3(256), 0, st, r, pts, n, S);
   kt_end(st);
 }
 
@@ -239,7 +239,7 @@ void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double 
   kt_begin("fk_n_kernel", st);
 #define IK_FKN(K)                                                                           \
   case K:                                                                                   \
-    hipLaunchKernelGGL(fk_n_kernel<K>, dim3(grid), dim3(256), 0, st, dh, ang, n, xyz, mats, S); \
+    IK_LAUNCH(fk_n_kernel<K>, dim3(grid), dim3(256), 0, st, dh, ang, n, xyz, mats, S); \
     break;
   switch (nj) {
     IK_FKN(2)
@@ -250,7 +250,7 @@ void launch_fk_n(int nj, const double *dh, const double *ang, int64_t n, double 
     IK_FKN(7)
     IK_FKN(8)
     default:
-      hipLaunchKernelGGL(fk_any_kernel, dim3(grid), dim3(256), 0, st, nj, dh, ang, n, xyz, mats, S);
+      IK_LAUNCH(fk_any_kernel, dim3(grid), dim3(256), 0, st, nj, dh, ang, n, xyz, mats, S);
       break;
   }
 #undef IK_FKN
@@ -272,7 +272,7 @@ void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, dou
   const unsigned grid_all = (unsigned)((n + 255) / 256);
   kt_begin("fk_kernel", st);
   if (joints) {
-    hipLaunchKernelGGL(fk_mats_kernel, dim3(grid_all), dim3(256), 0, st, r, ang, n, xyz,
+    IK_LAUNCH(fk_mats_kernel, dim3(grid_all), dim3(256), 0, st, r, ang, n, xyz,
                        joints, S);
   } else {
     FkConst kc;
@@ -285,7 +285,7 @@ void launch_fk(const RobotDev &r, const double *ang, int64_t n, double *xyz, dou
     // 1M points: at that size the launch's fixed cost, ~6 us, is a third of it)
     const unsigned cap = (unsigned)fk_cus() * 8;
     const unsigned grid = grid_all < cap ? grid_all : cap;
-    hipLaunchKernelGGL(fk_kernel, dim3(grid), dim3(256), 0, st, r, kc, ang, n, xyz, S);
+    IK_LAUNCH(fk_kernel, dim3(grid), dim3(256), 0, st, r, kc, ang, n, xyz, S);
   }
   kt_end(st);
 }

@@ -16,6 +16,9 @@ constexpr int kMaxTimed = 64;  // kernels timed per call (the layered ANN path l
 struct KTimer {
   bool on = false;
   int n = 0;
+  // slot n's state: 1 = armed by kt_begin (the next IK_LAUNCH takes its events),
+  // 2 = stamped by that dispatch, 3 = a marker span (kt_span_begin)
+  int state = 0;
   hipEvent_t beg[kMaxTimed] = {};
   hipEvent_t end[kMaxTimed] = {};
   const char *name[kMaxTimed] = {};

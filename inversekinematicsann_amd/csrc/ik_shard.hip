@@ -388,17 +388,20 @@ int auto_chunks(ik_ctx *c, int method, int64_t n) {
   const IkComm &m = c->comm;
   int C = m.chunks_req;
   if (C <= 0) C = env_chunks();
-  // automatic (DESIGN.md §5's gather model): ANN one chunk -- its gather is
-  // ~0.5 % of the solve, a second launch tail would cost more than the overlap
-  // saves; FABRIK two chunks at g > 1 -- its 32-byte rows gather in about the
-  // solve's time at 8 ranks, and chunk 0's gather then runs under chunk 1's
-  // solve (predicted 0.62 against 0.76 ms a step, configs[4] at 8 ranks).  The
-  // plan depends only on (n, g, method) and the explicit setting, so every rank
-  // makes the same one (ik_comm_init checks the environment's, every call's
-  // tail its plan); bench.py's gather check compares the gathered rows with a
-  // plain re-solve bit for bit on every N > 1 run.
+  // automatic: one chunk for both methods.  ANN's gather is ~0.5 % of the solve;
+  // FABRIK's 32-byte rows gather in about the solve's time at 8 ranks, and two
+  // chunks would overlap chunk 0's gather with chunk 1's solve (DESIGN.md §5's
+  // model: 0.93 against 1.06 ms a step for configs[4] at 8 ranks), but the
+  // chunked gather has run bit-checked only through the loopback communicator,
+  // never across real RCCL ranks, so it stays opt-in (ik_comm_set_chunks /
+  // IKHIP_GATHER_CHUNKS) until an N >= 2 run records its gather check (ADVICE
+  // r05).  The plan depends only on (n, g, method) and the explicit setting, so
+  // every rank makes the same one (ik_comm_init checks the environment's, every
+  // call's tail its plan); bench.py's gather check compares the gathered rows
+  // with a plain re-solve bit for bit on every N > 1 run.
   (void)n;
-  if (C <= 0) C = (method == IK_METHOD_FABRIK && m.nranks > 1) ? 2 : 1;
+  (void)method;
+  if (C <= 0) C = 1;
   return C > IK_MAX_GATHER_CHUNKS ? IK_MAX_GATHER_CHUNKS : C;
 }
 
@@ -489,7 +492,7 @@ int sharded_enqueue(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, in
     if (m.loopback) {
       const uint64_t tot = (uint64_t)cnt * g, blocks = (tot + 255) / 256;
       if (tot)
-        hipLaunchKernelGGL(loopback_gather_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)),
+        IK_LAUNCH(loopback_gather_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)),
                            dim3(256), 0, m.cs, static_cast<const uint8_t *>(send),
                            static_cast<uint8_t *>(recv), (uint64_t)cnt, g, me, replicate ? 1 : 0,
                            m.stall ? m.stall_flag : nullptr, cap_ticks);
@@ -545,7 +548,7 @@ int sharded_enqueue(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, in
       if (j.fk_err) {
         const int64_t want = (j.m + 2047) / 2048;
         kt_begin("fk_hist_kernel", c->stream);
-        hipLaunchKernelGGL(fk_hist_kernel, dim3((unsigned)(want < 512 ? want : 512)), dim3(256),
+        IK_LAUNCH(fk_hist_kernel, dim3((unsigned)(want < 512 ? want : 512)), dim3(256),
                            0, c->stream, j.fk_err, j.m, m.tail_send->hist);
         kt_end(c->stream);
       }
@@ -554,13 +557,13 @@ int sharded_enqueue(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, in
     }
     const bool last = k == C - 1;
     if (last) {
-      hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, m.tail_send);
+      IK_LAUNCH(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, m.tail_send);
     }
     IK_HIP(hipGetLastError());
     IK_HIP(hipEventRecord(m.ev_solved[k], c->stream));
     IK_HIP(hipStreamWaitEvent(m.cs, m.ev_solved[k], 0));
     // chunk k's rows of every rank, in place (+ every rank's tail block with the last)
-    kt_begin("rccl_all_gather", m.cs);
+    kt_span_begin("rccl_all_gather", m.cs);
     IK_HIP(hipEventRecord(m.ev_gs[k], m.cs));
     if ((rc = group(true))) return rc;
     for (int q = 0; q < nreg && !rc; ++q) {
@@ -584,7 +587,7 @@ int sharded_enqueue(ik_ctx *c, int method, const ik_shard_plan &P, Region *R, in
   if (C == 0) {  // an empty batch: every rank still exchanges its (empty) tail
     launch_reset_stats(m.d_cstats, c->stream);
     ta.K = 1;
-    hipLaunchKernelGGL(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, m.tail_send);
+    IK_LAUNCH(pack_tail_kernel, dim3(1), dim3(64), 0, c->stream, ta, m.tail_send);
     IK_HIP(hipGetLastError());
     IK_HIP(hipEventRecord(m.ev_solved[0], c->stream));
     IK_HIP(hipStreamWaitEvent(m.cs, m.ev_solved[0], 0));

@@ -23,6 +23,8 @@ def pb(s, e, d):
 
 def band(tol2, n1max, sum_l):
     """fabrik_band (ik_fabrik_step.h), restated."""
+    if not tol2 > 0.0:
+        return -1.0, np.inf, 0.0  # decides nothing: every comparison exact
     T = np.sqrt(tol2)
     tlo, thi = T * (1.0 - 2.0 ** -50), T * (1.0 + 2.0 ** -50)
     d = 2.0 ** -52 * (3.0 * n1max + 4.0 * sum_l + 1.0)
@@ -108,3 +110,40 @@ def test_band_decisions_match_exact_comparisons():
                 else:
                     undecided += 1
     assert checked > 5000 and undecided > 1000
+
+
+def test_band_at_tol_zero_decides_nothing():
+    """tol = 0 (tol2 = 0): fabrik.py:57 stops only where both errors are exactly 0.
+    A band with hi = 0 would call every lane with |1 - q| sqrt(x) > 0 "above tol",
+    also one whose b0 rounds exactly onto start (se2 == 0) while q is an ulp off 1
+    (not met on the trajectories below, where se2 == 0 comes with
+    q == 1, but nothing rules it out).  fabrik_band returns (lo, hi) = (-1, inf)
+    for tol2 <= 0, so no lane is decided by it and every comparison is exact;
+    tests/test_gpu_parity.py::test_fabrik_tol_zero_and_negative checks the kernels."""
+    import re
+    src = open(__file__.replace("tests/test_band_cpu.py",
+                                "inversekinematicsann_amd/csrc/ik_fabrik_step.h")).read()
+    body = src[src.index("fabrik_band(double tol2"):]
+    assert re.search(r"ErrBand b = \{-1\.0, INFINITY\};\s*(//[^\n]*\n\s*)*"
+                     r"if \(!\(tol2 > 0\.0\)\) return b;", body[:800]), \
+        "fabrik_band must decide nothing for tol2 <= 0"
+    rng = np.random.default_rng(7)
+    L = 2.0
+    J, g = chains(4000, rng)
+    g = J[0] + (g - J[0]) * 0.4  # mostly reachable goals, so chains converge
+    start, c1, c2 = J[0], J[1], J[2]
+    lo, hi, _ = band(0.0, 100.0, 8.0)
+    assert lo < 0.0 and hi == np.inf
+    zero = 0
+    for _ in range(100):
+        b2, _, _ = pb(g, c2, L)
+        b1, _, _ = pb(b2, c1, L)
+        b0, x, q = pb(b1, start, L)
+        se2 = ((b0 - start) ** 2).sum(1)
+        sea = np.abs(1.0 - q) * np.sqrt(x)
+        zero += int((se2 == 0.0).sum())
+        # at tol2 = 0 the band never claims a decision
+        assert not (sea > hi).any() and not (sea < lo).any()
+        c1, _, _ = pb(start, b1, L)
+        c2, _, _ = pb(c1, b2, L)
+    assert zero > 0  # converged chains do reach se2 == 0, where tol 0 can stop

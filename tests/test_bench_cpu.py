@@ -199,3 +199,74 @@ def test_strong_legs_are_configs_3_and_4_at_world_8():
     for w in (2, 4):
         assert bench._config_ref("ann", 10_000_000, w, 1e-3, 100) == "configs[3]"
         assert bench._config_ref("fabrik", 10_000_000, w, 1e-5, 200) == "configs[4]"
+
+
+def test_kernel_duration_longer_than_its_step_is_dropped():
+    """an events duration longer than the step that launched the
+    kernel is not a kernel duration; the roofline then rests on rocprof alone."""
+    import bench
+    assert bench.kernel_time_ok(0.30, 0.36) and not bench.kernel_time_ok(0.52, 0.51)
+    assert not bench.kernel_time_ok(None, 0.5) and not bench.kernel_time_ok(0.3, None)
+    fr = bench.roofline_fracs(100.0, 0.52, 1000.0, {"rocprof_avg_ms": 0.467}, step_ms=0.511)
+    assert fr["frac_events"] is None and not fr["kernel_ms_valid"]
+    assert fr["headline"] == "rocprof"
+    fr = bench.roofline_fracs(100.0, 0.47, 1000.0, {"rocprof_avg_ms": 0.467}, step_ms=0.511)
+    assert fr["kernel_ms_valid"] and fr["frac_events"] is not None
+
+
+def _lease_lines():
+    """Every bench line committed under profiles/r06 (one JSON object per file, or
+    JSON lines)."""
+    import glob
+    import json
+    out = []
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "r06", "**", "*bench*.json"),
+                              recursive=True)):
+        with open(p) as f:
+            txt = f.read().strip()
+        for ln in ([txt] if txt.startswith("{") and txt.count("\n{") == 0 else txt.splitlines()):
+            ln = ln.strip()
+            if ln.startswith("{"):
+                try:
+                    d = json.loads(ln)
+                except ValueError:
+                    continue
+                if "metric" in d and "ms_per_step" in d:
+                    out.append((p, d))
+    return out
+
+
+def test_committed_bench_lines_kernel_fits_step():
+    """in every committed r06 bench line, each method's roofline
+    kernel_ms (the dispatch-stamped events) fits inside its ms_per_step, and where
+    both figures exist frac_events is within 5 % of frac_rocprof."""
+    lines = _lease_lines()
+    for path, d in lines:
+        entries = [("headline", d)] + list(d.get("secondary", {}).items())
+        for name, e in entries:
+            rf, step = e.get("roofline") or {}, e.get("ms_per_step")
+            k = rf.get("kernel_ms")
+            if k is None or step is None:
+                continue
+            assert k <= step, (path, name, k, step)
+            fe, fr = rf.get("frac_events"), rf.get("frac_rocprof")
+            if fe and fr and name in ("headline", "fabrik", "fabrik_tol1e-5", "fk"):
+                assert abs(fe / fr - 1.0) <= 0.05, (path, name, fe, fr)
+
+
+def test_wall_budget_fits_the_driver_limit():
+    """`bench.py --gpus 8` (weak headline, secondaries, both strong
+    legs, gather checks, end-to-end, cold steps, start-up and RCCL init) fits the
+    driver's 600 s limit at its --steps 20 --warmup 5 and at the defaults, and so
+    does a run whose collective stalls until IKHIP_RCCL_TIMEOUT_S aborts it."""
+    import bench
+    for world in (1, 2, 4, 8):
+        for steps, warmup in ((20, 5), (10, 2)):
+            b = bench.wall_budget(world, steps, warmup)
+            assert b["total_s"] <= bench.DRIVER_TIMEOUT_S, (world, b)
+            assert b["stall_path_s"] <= bench.DRIVER_TIMEOUT_S, (world, b)
+            if world > 1:
+                assert {"ann_strong10M", "fabrik_tol1e-5_strong10M"} <= set(b["legs_s"])
+    # the library's default deadline (ik_shard.hip) is the one the budget assumes
+    src = open(os.path.join(ROOT, "inversekinematicsann_amd", "csrc", "ik_shard.hip")).read()
+    assert "env = v > 0.0 ? v : 120.0;" in src

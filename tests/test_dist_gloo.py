@@ -45,6 +45,29 @@ def _part_solve(pts, b, e, tol, mi):
     return ang, it, err, stats
 
 
+ANN_DIMS_SMALL = (3, 48, 48, 4)  # a small tanh MLP: the protocol, not the model, is tested
+
+
+def _ann_part_solve(pts, b, e):
+    """Rows [b, e) through the ANN oracle (ann.py:70-76 on a seeded Glorot model):
+    float32 angles, FK errors, and the stats pack_tail_kernel would record."""
+    from oracle import oracle as O
+    from inversekinematicsann_amd.kinematics.ann import (REFERENCE_X_SCALER as XS,
+                                                         REFERENCE_Y_SCALER as YS, glorot_model)
+    m = glorot_model(ANN_DIMS_SMALL, seed=4)
+    local = pts[b:e]
+    ang = O.ann_forward(local, m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean,
+                        YS.scale, compute=np.float32).astype(np.float32)
+    xyz, _, _ = O.fk(ang.astype(np.float64))
+    err = np.sqrt(((xyz - local) ** 2).sum(axis=1))
+    oob = O.check_limits(local) if len(local) else -1
+    stats = dict(first_oob=b + oob if oob >= 0 else -1, first_err=-1, first_err_code=0,
+                 max_iters=0, sum_iters=0, n_capped=0,
+                 max_fk_err=float(err.max()) if len(err) else 0.0, sum_fk_err=float(err.sum()),
+                 rows=len(local))
+    return ang, err, stats
+
+
 def _tail(parts_stats):
     """The rank's tail from its parts' stats in chunk order (pack_tail_kernel)."""
     from inversekinematicsann_amd import _native
@@ -64,7 +87,7 @@ def _tail(parts_stats):
     return t
 
 
-def _worker(rank, world, port, n, chunks, bad, q):
+def _worker(rank, world, port, n, chunks, bad, q, method="fabrik"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world))
     import ctypes
@@ -80,13 +103,18 @@ def _worker(rank, world, port, n, chunks, bad, q):
             pts[i] = v
         plan = _native.shard_plan(n, world, chunks)
         assert (plan.chunks, plan.part_rows, plan.full_rows) == D.plan_of(n, world, chunks)
-        ang = np.full((n, 4), -7.0)
+        ang = np.full((n, 4), -7.0, np.float32 if method == "ann" else np.float64)
         it = np.full(n, -7, np.int32)
         err = np.full(n, -7.0)  # only this rank's rows are written (stays local)
         stats = []
 
         def solve_part(b, e):
             assert (b, e) == _native.shard_part(plan, rank, len(stats))
+            if method == "ann":  # ik_ann_solve_sharded gathers the angles only
+                a, f, s = _ann_part_solve(pts, b, e)
+                err[b:e] = f
+                stats.append(s)
+                return [a]
             a, i, f, s = _part_solve(pts, b, e, 1e-3, 100)
             err[b:e] = f
             stats.append(s)
@@ -97,7 +125,8 @@ def _worker(rank, world, port, n, chunks, bad, q):
             dist.all_gather(out, torch.from_numpy(np.ascontiguousarray(send)))
             recv[...] = torch.cat(out).numpy()
 
-        parts = D.gather_in_place(n, world, rank, chunks, solve_part, [ang, it], all_gather)
+        outs = [ang] if method == "ann" else [ang, it]
+        parts = D.gather_in_place(n, world, rank, chunks, solve_part, outs, all_gather)
         assert len(parts) == plan.chunks
         while len(stats) < len(parts):  # empty parts record zero stats
             stats.append(dict(first_oob=-1, first_err=-1, first_err_code=0, max_iters=0,
@@ -124,15 +153,15 @@ def _worker(rank, world, port, n, chunks, bad, q):
         q.put((rank, repr(e) + traceback.format_exc()))
 
 
-def _run(world, n, chunks=1, bad=()):
+def _run(world, n, chunks=1, bad=(), method="fabrik"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, chunks, list(bad), q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, chunks, list(bad), q, method))
              for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
+    res = [q.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -237,3 +266,77 @@ def test_lowest_failing_index_across_shards():
             assert st["first_oob"] == 70
             assert st["first_err"] == 10 and st["first_err_code"] == 3
             assert np.isnan(ang[10]).all() and np.isnan(ang[80]).all()
+
+
+# ---- world 8: the driver's N = 8 run, rehearsed on the CPU ----
+
+def test_world8_fabrik_two_chunks_ragged():
+    """8 ranks, FABRIK, C = 2 chunks (the opt-in overlap; ik_comm_set_chunks) on a
+    ragged n = 10 007: S = 626, chunk 0 in place, chunk 1 staged (its last part
+    ragged, one rank's part empty); every rank ends with the single-process rows
+    bit for bit, the stats of the whole batch, and its own FK errors only."""
+    from inversekinematicsann_amd import dist as D
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    n, world, chunks = 10_007, 8, 2
+    C, S, full = D.plan_of(n, world, chunks)
+    assert (C, S) == (2, 626) and full < n  # a staged, ragged last chunk
+    pts = random_dist(n, seed=11)
+    ref_ang, ref_it, ref_err, ref_t = _part_solve(pts, 0, n, 1e-3, 100)
+    seen = np.zeros(n, np.int32)
+    res = _run(world, n, chunks)
+    assert [r[0] for r in res] == list(range(world))
+    for rank, ang, it, err, st, p99, parts in res:
+        assert np.array_equal(ang, ref_ang) and np.array_equal(it, ref_it), rank
+        assert len(parts) == C
+        mine = np.zeros(n, bool)
+        for b, e in parts:
+            mine[b:e] = True
+            seen[b:e] += 1
+        assert np.array_equal(err[mine], ref_err[mine], equal_nan=True)
+        assert (err[~mine] == -7.0).all()
+        assert st["sum_iters"] == ref_t["sum_iters"] and st["max_iters"] == ref_t["max_iters"]
+        assert st["n_capped"] == ref_t["n_capped"]
+        assert st["max_fk_err"] == ref_t["max_fk_err"]
+        assert p99 == D.hist_quantile([D.fkhist(ref_err)], 0.99)
+    assert (seen == 1).all()
+
+
+def test_world8_ann_one_chunk():
+    """8 ranks, ANN, C = 1 (the automatic plan): float32 angle rows (16 B) gathered
+    in place; every rank holds what one process computes for the same eight parts
+    bit for bit (the oracle's BLAS forward is row-invariant only for equal batch
+    shapes, so the reference solves the same parts)."""
+    from inversekinematicsann_amd import dist as D
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    n, world = 10_007, 8
+    pts = random_dist(n, seed=11)
+    ref_ang = np.empty((n, 4), np.float32)
+    ref_err = np.empty(n)
+    mx = 0.0
+    for r in range(world):
+        b, e = D.shard_bounds(n, world, r)
+        ref_ang[b:e], ref_err[b:e], t = _ann_part_solve(pts, b, e)
+        mx = max(mx, t["max_fk_err"])
+    res = _run(world, n, 1, method="ann")
+    for rank, ang, it, err, st, p99, parts in res:
+        assert ang.dtype == np.float32 and np.array_equal(ang, ref_ang), rank
+        assert len(parts) == 1 and parts[0] == D.shard_bounds(n, world, rank)
+        b, e = parts[0]
+        assert np.array_equal(err[b:e], ref_err[b:e])
+        assert st["first_oob"] == -1 and st["max_fk_err"] == mx
+        assert p99 == D.hist_quantile([D.fkhist(ref_err)], 0.99)
+
+
+def test_world8_lowest_failing_index():
+    """8 ranks: out-of-reach points on ranks 5 and 2 and ZeroDivision points on
+    ranks 7, 3 and 6 (n = 8 000, S = 1 000 at C = 1; 500 at C = 2): every rank
+    reports the lowest GLOBAL index of each kind (inverse.py:117 checks the whole
+    batch first; the reference then fails at the first bad point, point.py:40)."""
+    n = 8000
+    bad = [(5300, [1.0, 2.0, -4.0]), (2950, [7.0, 0.0, 1.0]),      # out of reach
+           (7100, [0.0, 0.0, 2.0]), (3001, [0.0, 0.0, 2.0]), (6999, [0.0, 0.0, 2.0])]
+    for chunks in (1, 2):
+        for _, ang, _, err, st, _, _ in _run(8, n, chunks, bad=bad):
+            assert st["first_oob"] == 2950
+            assert st["first_err"] == 3001 and st["first_err_code"] == 3
+            assert np.isnan(ang[3001]).all() and np.isnan(ang[7100]).all()

@@ -108,3 +108,40 @@ def test_bad_device_index():
     rc = L.ik_ctx_create(4096, ctypes.byref(h))
     assert rc == N.IK_E_BADARG and not h.value
     assert b"out of range" in L.ik_last_error()
+
+
+def test_ann_effective_mode_reports_the_arithmetic_run():
+    """ik_ann_effective_mode: the set mode when the model has layers
+    that take it, fp32 for a fused model wider than 512 (with a RuntimeWarning from
+    the Python wrapper), bf16x6 for fp16x3 on the layered path; -IK_E_NOMODEL
+    before a model is loaded."""
+    import warnings
+    from inversekinematicsann_amd import _native as N
+    from inversekinematicsann_amd.kinematics.ann import (REFERENCE_X_SCALER as XS,
+                                                         REFERENCE_Y_SCALER as YS, glorot_model)
+    c = N.Context(0)
+    try:
+        assert c.lib.ik_ann_effective_mode(c.handle) == -N.IK_E_NOMODEL
+
+        def load(dims):
+            m = glorot_model(dims, seed=1)
+            c.ann_load(m.weights, m.biases, m.activations, XS.mean, XS.scale, YS.mean, YS.scale)
+
+        load((3, 64, 64, 4))
+        for mode in ("fp32", "bf16x6", "fp16x3"):
+            c.ann_set_mode(mode)
+            assert c.ann_effective_mode() == mode
+        c.ann_set_mode("bf16x6")
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            load((3, 600, 600, 4))          # fused, wider than 512: fp32 build
+        assert c.ann_effective_mode() == "fp32"
+        assert any("ik_ann_effective_mode" in str(x.message) for x in w)
+        c.ann_set_mode("fp16x3")
+        load((3,) + (64,) * 30 + (4,))      # past the fused kernel's 24 layers: layered
+        assert c.ann_effective_mode() == "bf16x6"
+        pts = np.array([[1.0, 0.5, 2.0], [0.3, -0.2, 1.0]])
+        ang, _ = c.ann_solve(pts)[:2]
+        assert np.isfinite(ang).all()
+    finally:
+        c.close()

@@ -68,6 +68,23 @@ def test_fabrik_vs_oracle_random(ctx):
         assert np.abs(jo - rjo).max() <= 1e-9
 
 
+def test_fabrik_tol_zero_and_negative(ctx):
+    """tol = 0 (and tols whose threshold rounds to 0, or below it) is accepted by
+    the reference (fabrik.py:57: the loop stops only when both errors are exactly
+    0).  The kernels' error band must then decide nothing: a lane whose b0 lands
+    exactly on start (se2 == 0) while |1 - q| sqrt(x) > 0 stops with the reference
+    (ADVICE r05).  ~12 % of these points stop before the cap at tol 0."""
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    pts = random_dist(20_000, seed=11)
+    for tol, mi in ((0.0, 100), (1e-300, 100), (-1.0, 5)):
+        ang, it, jo, st = ctx.fabrik_solve(pts, tol, mi, want_joints=True)
+        rang, rit, rjo, rst = O.fabrik_ikine(pts, tol, mi)
+        assert np.array_equal(it, rit), (tol, int((it != rit).sum()))
+        assert np.abs(ang - rang).max() <= 1e-9, tol
+        assert np.abs(jo - rjo).max() <= 1e-9, tol
+    assert int((rit < 5).sum()) == 0
+
+
 def test_fabrik_ragged_sizes(ctx):
     from inversekinematicsann_amd.robot.position_generator import random_dist
     for n in (1, 63, 64, 65, 255, 257, 1000, 4097):
@@ -476,8 +493,9 @@ def test_ann_layered_bf16x6_kernel_runs(ctx1):
 
 def test_ann_layered_bf16x6_chunks(ctx1, monkeypatch):
     """bf16x6 through the layered path over many chunks (a 1 MiB activation budget;
-    the buffers hold three bf16 planes per element between split layers) equals one
-    chunk bit for bit and stays within 1e-5 of a float64 forward."""
+    the activation buffers hold fp32 rows, which annb_gemm_x6_kernel splits into
+    three bf16 parts in LDS as it stages them) equals one chunk bit for bit and
+    stays within 1e-5 of a float64 forward."""
     dims = (3, 1100, 300, 200, 4)
     try:
         ctx1.ann_set_mode("bf16x6")

@@ -49,9 +49,10 @@ METHODS_OF = {"ann_fused_kernel": ["ann"],
               "fk_kernel": ["fk"]}
 
 
-# bench.timed(): the per-kernel event step between the warm-up and the timed loop
-# (--event-steps; profiles/r05/lease_f was made by a bench with one more, untimed)
-EVENT_STEPS = 1
+# bench.timed(): the per-kernel event steps between the warm-up and the timed loop
+# (--event-steps: bench.TIMING_REPS from r06, 1 before; profiles/r05/lease_f was
+# made by a bench with one more, untimed)
+EVENT_STEPS = 5
 
 
 def _rows(d, pat):
