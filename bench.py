@@ -588,6 +588,10 @@ def run_fabrik(job, args, tol=None, max_iter=None):
         res["gather_check"] = gather_check(job, {"ang": dang, "iters": dit}, resolve)
     if args.cold:
         res["cold"] = cold_steps(ctx, step)
+        if job.sc is None:
+            # the same cold call on batches of other distributions:
+            # the built-in table was learned on random_dist only
+            res["cold"]["other_distributions"] = cold_other(ctx, job.n_local, tol, max_iter)
     n = job.n_local
     res["mean_iters"] = sum_iters / job.total
     res["n_capped"] = int(n_capped)
@@ -700,20 +704,23 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
     # per-kernel durations: the library launches each kernel of a timed call with
     # hipExtLaunchKernel's start / stop events, which the dispatch itself stamps
     # (ik_ctx_set_timing), so a kernel's interval holds neither the
-    # kernels ahead of it in the step nor the host's launch latency.  Median of
-    # TIMING_REPS single steps, each from an idle queue.
-    ctx.set_timing(True)
+    # kernels ahead of it in the step nor the host's launch latency.  Each timed
+    # step is enqueued right behind an untimed one, as in the timed loop (a step
+    # from an idle queue ran its kernels 3-6 % slower than the loop's); median of
+    # TIMING_REPS such steps.
     per = {}
     for _ in range(TIMING_REPS):
+        step()
+        ctx.set_timing(True)
         step()
         ctx.sync()
         one = {}
         for name, ms in ctx.kernel_times():
             one[name] = one.get(name, 0.0) + ms
+        ctx.set_timing(False)
         for name, ms in one.items():
             per.setdefault(name, []).append(ms)
     kernels = {name: float(np.median(v)) for name, v in per.items()}
-    ctx.set_timing(False)
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -769,6 +776,54 @@ def cold_steps(ctx, step, reps=3):
             "note": "fresh-context call: work-order table reset to the built-in SixDOFRobot "
                     "table before each call (ik_fabrik_reset_order); empty_table: point order; "
                     "warm = ms_per_step (its table learned on a warm-up batch of another seed)"}
+
+
+def cold_batches(n):
+    """The cold call's other inputs: n points of the uniform
+    workspace box (the reference's random_distribution('uniform'),
+    position_generator.py:91-92, drawn vectorised with a seeded generator: 37 % of
+    them out of reach, capped) and an n-point spring trajectory (the CLI's
+    --shape spring, position_generator.py:73-78, with the cli.py:195 example's
+    shape arguments 2, 3, 6): consecutive points of one smooth curve, so point
+    order runs through easy and hard stretches in long runs."""
+    from inversekinematicsann_amd.robot.position_generator import spring
+    from inversekinematicsann_amd.robot.robot import SixDOFRobot
+    lim = SixDOFRobot.effector_workspace_limits
+    rng = np.random.default_rng(5)
+    box = np.stack([rng.uniform(float(lo), float(hi), n) for lo, hi in lim.values()], axis=1)
+    return {"uniform_box": box, "spring": spring(n, 2, 3, 6)}
+
+
+def cold_other(ctx, n, tol, max_iter, reps=3):
+    """cold_steps on each of cold_batches(n): a fresh context's table (the
+    built-in one) against an empty table (point order), median of `reps` each,
+    with the iteration counts of both compared (the order must not change them)."""
+    import torch
+    out = {}
+    for name, pts in cold_batches(n).items():
+        dp = torch.from_numpy(pts).cuda()
+        ang = torch.empty((n, 4), dtype=torch.float64, device="cuda")
+        it = torch.empty(n, dtype=torch.int32, device="cuda")
+        err = torch.empty(n, dtype=torch.float64, device="cuda")
+
+        def step():
+            ctx.fabrik_solve_device(dp, ang, it, None, tol, max_iter, fk_err=err)
+        step()  # scratch sized for this batch
+        ctx.sync()
+        c = cold_steps(ctx, step, reps)
+        it_prior = it.clone()
+        ctx.fabrik_order_set(None)
+        step()
+        ctx.sync()
+        same = bool(torch.equal(it, it_prior))
+        ctx.fabrik_reset_order()
+        out[name] = {"ms": c["ms"], "all_ms": c["all_ms"], "empty_table_ms": c["empty_table_ms"],
+                     "empty_table_all_ms": c["empty_table_all_ms"],
+                     "prior_over_empty": c["ms"] / c["empty_table_ms"],
+                     "iters_equal_across_orders": same,
+                     "mean_iters": float(it.double().mean().item())}
+        del dp, ang, it, err
+    return out
 
 
 def end_to_end(job, solve_host, args):

@@ -51,6 +51,30 @@ constexpr bool kWide = false;
 constexpr int kWaves = 4;  // waves per workgroup
 constexpr int kHPad = 64;  // floats past the last activation row (see layer_gemm)
 
+// Row layout of the activation tile H (LY).  0: row r at r kLd floats (kLd = 516:
+// row r starts one 16-byte slot after row r - 1).  1, the bf16x6 kernel's: a stride
+// of kLdX = 520 floats (130 slots, 2 mod 16) and rows 4..11 of every 16 one slot
+// further, so row r starts at slot 2r + [r mod 16 in 4..11] (mod 16): rows 0-3 and
+// 12-15 of a 16-row block on even slots, rows 4-11 on odd ones.  Its K loop
+// (layer_gemm_x16) reads with ds_read_b128, lane (row lane & 15, k-block lane >> 4),
+// in the 16-lane groups {0-3, 12-15, 20-27}, {4-11, 16-19, 28-31}, ...
+// (MI355X_MICROARCH.md §LDS): a group takes rows 0-3, 12-15 of one k-block and rows
+// 4-11 of the next (2 slots on), 16 distinct slots; with kLd = 516 rows r and r + 2
+// of neighbouring k-blocks collided in every group (2-way, 39 % of LDS-active
+// cycles in the r05 profile).  Its epilogue stores (ds_write_b128, 8-lane groups of
+// 8 consecutive rows, banks mod 32 dwords = 8 slots) land on 8 distinct slots too,
+// and so do the fp32 GEMM's A reads of its first and last layers.  Row offsets that
+// are multiples of 16 rows add a multiple of 16 kLdX, so the per-lane bases stay
+// additive.
+constexpr int kLdX = kLd + 4;
+template <int LY>
+constexpr int ld_of() { return LY ? kLdX : kLd; }
+template <int LY>
+__device__ __forceinline__ int hrow(int r) {
+  if constexpr (LY != 0) return r * kLdX + ((((r + 4) >> 3) & 1) << 2);
+  else return r * kLd;
+}
+
 struct AnnArgs {
   AnnModelDev m;
   RobotDev r;
@@ -224,13 +248,13 @@ __device__ __forceinline__ void mma_group(const Frag<MR, NR> &f, f32x16 (&acc)[M
 #endif
 constexpr int kRing = IKHIP_ANN_RING;
 
-template <int MR, int NR>
+template <int MR, int NR, int LY = 0>
 __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restrict__ wp, int G,
                                            int wbytes, int g0, int g1, int nt0, int nt_stride,
                                            int lane, f32x16 (&acc)[MR][NR],
                                            unsigned long long *st_first = nullptr) {
   const int r = lane & 31, h = lane >> 5;
-  const float *ap = H + r * kLd + 4 * h;
+  const float *ap = H + hrow<LY>(r) + 4 * h;
 #pragma unroll
   for (int j = 0; j < NR; ++j)
 #pragma unroll
@@ -248,7 +272,7 @@ __device__ __forceinline__ void layer_gemm(const float *H, const f32x4 *__restri
   auto load_a = [&](Frag<MR, NR> &fr, const float *a0, int u) {
 #pragma unroll
     for (int m = 0; m < MR; ++m)
-      fr.a[m] = *reinterpret_cast<const f32x4 *>(a0 + m * 32 * kLd + 8 * u);
+      fr.a[m] = *reinterpret_cast<const f32x4 *>(a0 + m * 32 * ld_of<LY>() + 8 * u);
   };
 #pragma unroll
   for (int u = 0; u < kRing - 1; ++u) {  // group by group, as the loop issues them
@@ -322,7 +346,8 @@ __device__ __forceinline__ void store_h1(float *H, int row, int col, float v) {
 // transposed form below (bias in the accumulators, b128 stores) measured
 // 0.6 k cycles per layer slower here: its 5.9 k-cycle epilogue saves 0.7 k,
 // its GEMM loses 1.3 k (bias loads ahead of the first MFMA).
-template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
+// HOUT: 0 fp32 rows (in the LY layout), 1 fp16x3 split planes.
+template <int MR, int NR, int ACT, int HOUT = 0, int W = kWaves, int LY = 0>
 __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], int wave, int lane,
                                               f32x16 (&acc)[MR][NR], unsigned long long *st) {
   const int r = lane & 31, h = lane >> 5;
@@ -344,12 +369,12 @@ __device__ __forceinline__ void layer_store_c(float *H, const float (&bv)[NR], i
         for (int k = 0; k < 4; ++k) {
           const int q = q0 + 2 * k;
           const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;  // row of q + 1 is row + 1
-          if constexpr (HOUT) {
+          if constexpr (HOUT == 1) {
             store_h1(H, row, col, t[k].x);
             store_h1(H, row + 1, col, t[k].y);
           } else {
-            H[row * kLd + col] = t[k].x;
-            H[(row + 1) * kLd + col] = t[k].y;
+            H[hrow<LY>(row) + col] = t[k].x;
+            H[hrow<LY>(row + 1) + col] = t[k].y;
           }
         }
       }
@@ -575,7 +600,7 @@ __device__ __forceinline__ void layer_gemm_h16(const float *H, const f16x8 *__re
 // Epilogue of an fp16x3 layer in the 16x16 sub-tile layout above: per lane and
 // sub-tile four consecutive features of one point, one 8-byte store per plane
 // (or one ds_write_b128 of fp32).
-template <int MR, int NR, int ACT, bool HOUT = false, int W = kWaves>
+template <int MR, int NR, int ACT, int HOUT = 0, int W = kWaves, int LY = 0>
 __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
                                                 f32x16 (&acc)[MR][NR], unsigned long long *st,
                                                 float pre = 1.0f) {
@@ -599,8 +624,8 @@ __device__ __forceinline__ void layer_store_h16(float *H, int wave, int lane,
         for (int ph = 0; ph < 2; ++ph) {
           const int row = m * 32 + 16 * ph + (lane & 15);
           const f32x4 v = {t[2 * ph].x, t[2 * ph].y, t[2 * ph + 1].x, t[2 * ph + 1].y};
-          if constexpr (HOUT) store_h4(H, row, col, v);
-          else *reinterpret_cast<f32x4 *>(H + row * kLd + col) = v;
+          if constexpr (HOUT == 1) store_h4(H, row, col, v);
+          else *reinterpret_cast<f32x4 *>(H + hrow<LY>(row) + col) = v;
         }
       }
     }
@@ -636,7 +661,7 @@ __device__ __forceinline__ void load_ax16(f32x8 (&a)[MR][2], const float *ap, in
   for (int m = 0; m < MR; ++m)
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
-      const f32x4 *q = reinterpret_cast<const f32x4 *>(ap + (m * 32 + 16 * ph) * kLd + 32 * g);
+      const f32x4 *q = reinterpret_cast<const f32x4 *>(ap + (m * 32 + 16 * ph) * kLdX + 32 * g);
       const f32x4 lo4 = q[0], hi4 = q[1];
       a[m][ph] = f32x8{lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
     }
@@ -695,7 +720,8 @@ template <int MR, int NR, int W = kWaves>
 __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__restrict__ wx,
                                                int G32, int xbytes, int wave, int lane,
                                                const float *bias, f32x16 (&acc)[MR][NR]) {
-  const float *ap = H + (lane & 15) * kLd + 8 * (lane >> 4);
+  // (the bf16x6 kernel's tile layout, LY 1)
+  const float *ap = H + hrow<1>(lane & 15) + 8 * (lane >> 4);
   f32x4 bl[NR][2];  // before the weights (layer_gemm_h16)
 #pragma unroll
   for (int j = 0; j < NR; ++j)
@@ -746,32 +772,32 @@ __device__ __forceinline__ void layer_gemm_x16(const float *H, const bf16x8 *__r
 // 2 fp16x3; wx: the layer's split weight operand in that mode, or nullptr for
 // a layer that stays fp32.  HX: the kernel runs fp16x3 layers, so hout (the next
 // layer is one) stores the activations as split planes.
-template <int ACT, bool HOUT, int W, int X, int MR, int NR>
+template <int ACT, int HOUT, int W, int X, int LY, int MR, int NR>
 __device__ __forceinline__ void store_any(bool tr, float *H, const float (&bv)[NR], int wave,
                                           int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st, float pre) {
   if (tr) {
-    if constexpr (X != 0) layer_store_h16<MR, NR, ACT, HOUT, W>(H, wave, lane, acc, st, pre);
+    if constexpr (X != 0) layer_store_h16<MR, NR, ACT, HOUT, W, LY>(H, wave, lane, acc, st, pre);
   } else {
-    layer_store_c<MR, NR, ACT, HOUT, W>(H, bv, wave, lane, acc, st);
+    layer_store_c<MR, NR, ACT, HOUT, W, LY>(H, bv, wave, lane, acc, st);
   }
 }
 
 // pre: the fp16x3 16x16x32 GEMM's accumulators still carry the weight pre-scale
 // (layer_gemm_h16); 1 for every other layer.
-template <bool HOUT, int W, int X, int MR, int NR>
+template <int HOUT, int W, int X, int LY, int MR, int NR>
 __device__ __forceinline__ void store_act(int act, bool tr, float *H, const float (&bv)[NR],
                                           int wave, int lane, f32x16 (&acc)[MR][NR],
                                           unsigned long long *st, float pre = 1.0f) {
   switch (act) {
-    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
-    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
-    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
-    default: store_any<IK_ACT_LINEAR, HOUT, W, X>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_TANH: store_any<IK_ACT_TANH, HOUT, W, X, LY>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_RELU: store_any<IK_ACT_RELU, HOUT, W, X, LY>(tr, H, bv, wave, lane, acc, st, pre); break;
+    case IK_ACT_SIGMOID: store_any<IK_ACT_SIGMOID, HOUT, W, X, LY>(tr, H, bv, wave, lane, acc, st, pre); break;
+    default: store_any<IK_ACT_LINEAR, HOUT, W, X, LY>(tr, H, bv, wave, lane, acc, st, pre); break;
   }
 }
 
-template <int MR, int NR, int X = 0, bool HX = false, int W = kWaves>
+template <int MR, int NR, int X = 0, int HX = 0, int W = kWaves, int LY = 0>
 __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float *bias, int act,
                                           int G, int wbytes, int wave, int lane, unsigned long long *st,
                                           unsigned long long *st_first,
@@ -791,25 +817,25 @@ __device__ __forceinline__ void run_layer(float *H, const f32x4 *wp, const float
   } else {
 #pragma unroll
     for (int j = 0; j < NR; ++j) bv[j] = bias[(wave + W * j) * 32 + (lane & 31)];
-    layer_gemm<MR, NR>(H, wp, G, wbytes, 0, G, wave, W, lane, acc, st_first);
+    layer_gemm<MR, NR, LY>(H, wp, G, wbytes, 0, G, wave, W, lane, acc, st_first);
   }
   const float pre = (X == 2 && tr) ? xinv : 1.0f;
-  if (HX && hout) store_act<true, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
-  else store_act<false, W, X>(act, tr, H, bv, wave, lane, acc, st, pre);
+  if (HX && hout) store_act<HX, W, X, LY>(act, tr, H, bv, wave, lane, acc, st, pre);
+  else store_act<0, W, X, LY>(act, tr, H, bv, wave, lane, acc, st, pre);
 }
 
-// HOUT: the next layer runs fp16x3, so the result goes out as split planes
+// HOUT 1: the next layer runs fp16x3, so the result goes out as split planes
 // (bytes [0, 64) and [1024, 1088) of the row: clear of the partials at floats
 // 32..159, which other threads of the block are still reading).
-template <int BM, int ACT, bool HOUT = false, int W = kWaves>
+template <int BM, int ACT, int HOUT = 0, int W = kWaves, int LY = 0>
 __device__ __forceinline__ void splitk_finish(float *H, const float *__restrict__ bias, int tid) {
   for (int o = tid; o < BM * 32; o += W * 64) {
     const int row = o >> 5, col = o & 31;
-    const float *p = H + row * kLd + 32 + col;
+    const float *p = H + hrow<LY>(row) + 32 + col;
     float v = ((p[0] + p[32]) + p[64]) + p[96];  // fixed order: deterministic
     const float y = act_apply<ACT>(v + bias[col]);
-    if constexpr (HOUT) store_h1(H, row, col, y);
-    else H[row * kLd + col] = y;
+    if constexpr (HOUT == 1) store_h1(H, row, col, y);
+    else H[hrow<LY>(row) + col] = y;
   }
 }
 
@@ -817,7 +843,7 @@ __device__ __forceinline__ void splitk_finish(float *H, const float *__restrict_
 // ann.py:56): the K range is split over the 4 waves, the partial BM x 32 tiles
 // go to LDS columns 32..159 (never read by this or the next layer) and are
 // summed in a fixed order, so no wave idles.
-template <int MR, bool HX = false, int W = kWaves>
+template <int MR, int HX = 0, int W = kWaves, int LY = 0>
 __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, const float *bias,
                                                  int act, int G, int wave, int lane, int tid,
                                                  unsigned long long *st, bool hout = false) {
@@ -827,7 +853,7 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
   // further waves only join the barriers)
   const int ws = wave < 4 ? wave : 4;
   const int g0 = (G * ws) / 4, g1 = wave < 4 ? (G * (wave + 1)) / 4 : g0;
-  layer_gemm<MR, 1>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, acc);
+  layer_gemm<MR, 1, LY>(H, wp, G, G * 1024, g0, g1, 0, 0, lane, acc);
   stamp(st);
   __syncthreads();
   const int r = lane & 31, h = lane >> 5;
@@ -837,25 +863,25 @@ __device__ __forceinline__ void run_layer_splitk(float *H, const f32x4 *wp, cons
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int row = m * 32 + (q & 3) + 8 * (q >> 2) + 4 * h;
-      H[row * kLd + 32 + wave * 32 + r] = acc[m][0][q];
+      H[hrow<LY>(row) + 32 + wave * 32 + r] = acc[m][0][q];
     }
   __syncthreads();
   switch (act) {
     case IK_ACT_TANH:
-      if (HX && hout) splitk_finish<BM, IK_ACT_TANH, true, W>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_TANH, false, W>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_TANH, HX, W, LY>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_TANH, 0, W, LY>(H, bias, tid);
       break;
     case IK_ACT_RELU:
-      if (HX && hout) splitk_finish<BM, IK_ACT_RELU, true, W>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_RELU, false, W>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_RELU, HX, W, LY>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_RELU, 0, W, LY>(H, bias, tid);
       break;
     case IK_ACT_SIGMOID:
-      if (HX && hout) splitk_finish<BM, IK_ACT_SIGMOID, true, W>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_SIGMOID, false, W>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_SIGMOID, HX, W, LY>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_SIGMOID, 0, W, LY>(H, bias, tid);
       break;
     default:
-      if (HX && hout) splitk_finish<BM, IK_ACT_LINEAR, true, W>(H, bias, tid);
-      else splitk_finish<BM, IK_ACT_LINEAR, false, W>(H, bias, tid);
+      if (HX && hout) splitk_finish<BM, IK_ACT_LINEAR, HX, W, LY>(H, bias, tid);
+      else splitk_finish<BM, IK_ACT_LINEAR, 0, W, LY>(H, bias, tid);
       break;
   }
 }
@@ -897,8 +923,12 @@ __global__ __launch_bounds__((64 * ann_waves<MR, X>()), (MR == 2 || kWide) ? 1 :
 ann_fused_kernel(AnnArgs a) {
   constexpr int BM = 32 * MR;
   constexpr int W = ann_waves<MR, X>();
+  // how a layer stores activations its split-GEMM successor reads (HOUT: fp16x3
+  // planes), and the tile's row layout (LY 1 for bf16x6)
+  constexpr int HK = X == 2 ? 1 : 0;
+  constexpr int LY = X == 1 ? 1 : 0;
   // + kHPad: the fp32 GEMM's operand ring reads up to 3 K groups past a row's end
-  __shared__ __attribute__((aligned(16))) float H[BM * kLd + kHPad];
+  __shared__ __attribute__((aligned(16))) float H[BM * ld_of<LY>() + kHPad];
   const int tid = threadIdx.x;
   // wave index in an SGPR: the per-wave column-tile count (cnt) and the paths it
   // selects are uniform branches, not exec-masked regions
@@ -937,7 +967,7 @@ ann_fused_kernel(AnnArgs a) {
         x1 = (float)((py - a.m.xm[1]) / a.m.xs[1]);
         x2 = (float)((pz - a.m.xm[2]) / a.m.xs[2]);
       }
-      f32x4 *row = reinterpret_cast<f32x4 *>(H + tid * kLd);
+      f32x4 *row = reinterpret_cast<f32x4 *>(H + hrow<LY>(tid));
       row[0] = f32x4{x0, x1, x2, 0.0f};
       row[1] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
@@ -964,33 +994,33 @@ ann_fused_kernel(AnnArgs a) {
       const bool hout = X == 2 && l + 1 < a.m.n_layers && a.m.wx[l + 1] &&
                         (a.m.np[l + 1] >> 5) > 1;
       if (NT == 1) {
-        run_layer_splitk<MR, X == 2, W>(HL, wp, bias, act, G, wave, lane, tid, sl, hout);
+        run_layer_splitk<MR, HK, W, LY>(HL, wp, bias, act, G, wave, lane, tid, sl, hout);
       } else if (X && wx) {
         const float xinv = a.m.xinv[l];
         const int G32 = (a.m.kp[l] + 31) >> 5;  // 32-deep K steps of the split GEMM
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, X, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout);
             break;
           case 3:
-            if constexpr (W * 3 <= 16) run_layer<MR, 3, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout);
+            if constexpr (W * 3 <= 16) run_layer<MR, 3, X, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout);
             break;
-          case 2: run_layer<MR, 2, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout); break;
-          case 1: run_layer<MR, 1, X, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout); break;
+          case 2: run_layer<MR, 2, X, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout); break;
+          case 1: run_layer<MR, 1, X, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, wx, G32, xinv, hout); break;
           default: __syncthreads(); break;
         }
       } else {
         const int cnt = (wave < NT) ? (NT - wave + W - 1) / W : 0;
         switch (cnt) {
           case 4:
-            if constexpr (W * 4 <= 16) run_layer<MR, 4, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
+            if constexpr (W * 4 <= 16) run_layer<MR, 4, 0, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
             break;
           case 3:
-            if constexpr (W * 3 <= 16) run_layer<MR, 3, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
+            if constexpr (W * 3 <= 16) run_layer<MR, 3, 0, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout);
             break;
-          case 2: run_layer<MR, 2, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
-          case 1: run_layer<MR, 1, 0, X == 2, W>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 2: run_layer<MR, 2, 0, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
+          case 1: run_layer<MR, 1, 0, HK, W, LY>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf, nullptr, 0, 1.0f, hout); break;
 #ifdef IKHIP_ANN_WIDE
           case 8: run_layer<MR, 8>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
           case 7: run_layer<MR, 7>(HL, wp, bias, act, G, G * NT * 1024, wave, lane, sl, sf); break;
@@ -1010,7 +1040,7 @@ ann_fused_kernel(AnnArgs a) {
       bool valid = pt < a.n;
       double err = 0.0;
       if (valid) {
-        const float *row = H + tid * kLd;
+        const float *row = H + hrow<LY>(tid);
         float y[4];
         double th[4];
 #pragma unroll

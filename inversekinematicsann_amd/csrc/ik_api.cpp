@@ -190,7 +190,8 @@ int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_it
   if (!S) S = c->d_stats;
   // a table still holding a built-in prior takes the one for this call's
   // tolerance; the solve then folds its own records in (learned from here on)
-  if (c->fab_prior >= 0 && n > 0) {
+  const bool prior = c->fab_prior >= 0 && n > 0;
+  if (prior) {
     if (prior_for(tol, max_iter) != c->fab_prior) {
       const int rc = seed_order(c, tol, max_iter);
       if (rc) return rc;
@@ -200,7 +201,7 @@ int fabrik_launch(ik_ctx *c, const double *dp, int64_t n, double tol, int max_it
   launch_reset_stats(S, c->stream);
   launch_fabrik_ikine(c->robot, dp, n, tol, max_iter, da, di, dj, dfe, limits, work, S,
                       c->stream, c->fabrik_variant, c->fabrik_core, c->fab_ord, c->rconst,
-                      c->dbg, c->fabrik_bpc);
+                      c->dbg, c->fabrik_bpc, prior);
   IK_HIP(hipGetLastError());
   return IK_OK;
 }

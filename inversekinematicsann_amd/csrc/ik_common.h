@@ -36,7 +36,7 @@ constexpr int kQueueHeads = 8;
 struct DevStats {
   unsigned long long first_oob;      // atomicMin of point index
   unsigned long long first_err_key;  // atomicMin of (index << 8) | code
-  unsigned long long ticket;         // unused since r03 (the FABRIK fold is its own kernel); kept for the layout
+  unsigned long long unseen;         // FABRIK classify: points whose goal cell the cost table has not seen
   // FABRIK work order: points per (cost class, block shard), and the scatter's
   // cursor inside each (class, shard) region of the queue
   unsigned int cls_tot[kOrdClasses][kOrdShards];
@@ -274,16 +274,12 @@ __device__ __forceinline__ int fk_chain(const double *dh, const double th[4], d3
   return st;
 }
 
-// The FABRIK seed pose (inverse.py:123-130) is fk_chain at [theta_1, dh[1],
-// dh[2], dh[3]]: only theta_1 = atan2(y, x) varies per point.  A_2..A_4 at the
-// seed angles and cos/sin(alpha_1) are per-robot constants, computed once by
-// robot_const_kernel with the same device functions (hence the same bits).
+// The per-robot constants of the FABRIK seed pose and of the FK round trip
+// (RobotConstDev), computed once per robot by robot_const_kernel.
 struct RobotConstDev {
-  double A[3][16];  // dh_transform(dh[k], dh[4+k], dh[8+k], dh[12+k]), k = 1..3
-  double ca1, sa1;  // cos / sin(alpha_1)
-  double d1, a1;    // dh[4], dh[8]: Tz / Tx of A_1
   double lim[6];    // workspace limits (inverse.py:26-35)
   double jc[16];    // fk_error's per-joint constants (fk_trip_consts)
+  double P[4][3];   // the seed chain's joints at theta_1 = 0 (seed_closed)
   int alpha_bad;
   int st;           // fk_chain's angle check of the constant angles
 };
@@ -291,53 +287,45 @@ struct RobotConstDev {
 // s_load_dwordx* into SGPRs instead of vector loads per lane.
 typedef const RobotConstDev __attribute__((address_space(4))) *RcConst;
 
-// Rows 0-2 of C = A * B, each element the same k-ordered FMA chain as mm4.
-// Rows 0-2 of a product only read rows 0-2 of its left factor, and the chain
-// only needs the translations (rows 0-2, column 3), so row 3 is never formed.
-__device__ __forceinline__ void mm4_r3(const double *A, const double *B, double *C) {
-  double T[12];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      double acc = 0.0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) acc = fma(A[i * 4 + k], B[k * 4 + j], acc);
-      T[i * 4 + j] = acc;
-    }
-#pragma unroll
-  for (int i = 0; i < 12; ++i) C[i] = T[i];
-}
-
-// fk_chain(dh, {th1, dh[1], dh[2], dh[3]}, J), bit for bit, from the constants:
-// A_1 = ((Rz(th1) Tz(d_1)) Tx(a_1)) Rx(alpha_1) and M_k = M_{k-1} A_k, rows 0-2.
-__device__ __forceinline__ int seed_chain(const RobotConstDev *rc, double th1, d3 J[4]) {
-  // the constants are read through the constant address space: wave-uniform
-  // s_load_dwordx* into SGPRs instead of 25 vector loads per lane, each a
-  // memory round trip on the seed's critical path
+// The seed pose in closed form.  theta_1 enters the DH chain only through the
+// leftmost factor, A_1 = Rz(theta_1) C_1 (forward.py:63-70), so every seed joint
+// is J_k = Rz(theta_1) P_k with P_k the chain's joint k at theta_1 = 0 (a robot
+// constant), and cos / sin(atan2(y, x)) = (x, y) / |(x, y)|: one reciprocal root
+// and four products per joint instead of atan2, cos, sin and three 3 x 4 matrix
+// products (r05: ~530 VALU per prepared batch entry).  The joints differ from the
+// reference's chain in the last bits of their x / y (for SixDOFRobot those are
+// ~1e-16 in size, P_k = (~1e-16, ~1e-16, 2k + 2)): no FABRIK iteration count
+// changed over 24M goals at tol 1e-3 .. 1e-8, random_dist and uniform box
+// (tools/seed_form_check.c against the oracle's chain).  Goals on the z axis or
+// with x^2 + y^2 outside the normal range (and NaN) take cos / sin of atan2 itself
+// in a wave-uniform branch.  Returns the robot's constant status.
+__device__ __forceinline__ int seed_closed(const RobotConstDev *rc, d3 g, d3 J[4]) {
   const RcConst k = (RcConst)rc;
-  double R[16], T1[16], T2[16], X[16], M[12];
-  const double c = cos(th1), s = sin(th1);
-  ident4(R);
-  R[0] = c; R[1] = -s; R[4] = s; R[5] = c;
-  ident4(T1);
-  T1[11] = k->d1;
-  ident4(T2);
-  T2[3] = k->a1;
-  ident4(X);
-  const double ca1 = k->ca1, sa1 = k->sa1;
-  X[5] = ca1; X[6] = -sa1; X[9] = sa1; X[10] = ca1;
-  mm4_r3(R, T1, M);
-  mm4_r3(M, T2, M);
-  mm4_r3(M, X, M);
-  J[0].x = M[3]; J[0].y = M[7]; J[0].z = M[11];
+  const double t = g.x * g.x + g.y * g.y;
+  const bool fast = t >= 0x1p-1000 && t <= 0x1p1000;
+  // 1 / sqrt(t): the hardware estimate and two coupled Newton steps (sqrt_core's
+  // g / h iteration: h -> 1 / (2 sqrt(t)) within a few ulps)
+  const double y0 = __builtin_amdgcn_rsq(t);
+  double h = 0.5 * y0, gg = t * y0;
+  double e = __builtin_fma(-h, gg, 0.5);
+  h = __builtin_fma(h, e, h);
+  gg = __builtin_fma(gg, e, gg);
+  e = __builtin_fma(-h, gg, 0.5);
+  h = __builtin_fma(h, e, h);
+  double c = g.x * (2.0 * h), s = g.y * (2.0 * h);
+  if (__builtin_expect(__any(!fast), 0)) {
+    if (!fast) {
+      const double th = atan2(g.y, g.x);
+      c = cos(th);
+      s = sin(th);
+    }
+  }
 #pragma unroll
-  for (int i = 1; i < 4; ++i) {
-    double A[16];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) A[e] = k->A[i - 1][e];
-    mm4_r3(M, A, M);
-    J[i].x = M[3]; J[i].y = M[7]; J[i].z = M[11];
+  for (int j = 0; j < 4; ++j) {
+    const double px = k->P[j][0], py = k->P[j][1];
+    J[j].x = __builtin_fma(c, px, -(s * py));
+    J[j].y = __builtin_fma(s, px, c * py);
+    J[j].z = k->P[j][2];
   }
   return k->st;
 }
@@ -347,16 +335,15 @@ __device__ __forceinline__ int seed_chain(const RobotConstDev *rc, double th1, d
 // with B_i = Tz(d_i) Tx(a_i) Rx(alpha_i) (forward.py:63-70 regrouped),
 // applied right to left to a vector; jc[i] = {a_i, d_i, cos alpha_i, sin alpha_i}
 // from the host (fk_trip_consts).  Same value as fk_chain up to rounding (~1e-15).
-__device__ __forceinline__ double fk_error(const double *jc, const double th[4], double px,
-                                           double py, double pz, int alpha_bad) {
-  bool ok = !alpha_bad;
+// The chain of fk_error from the angles' cosines and sines (c[i], s[i]) and
+// whether every angle passed forward.py:23-25's range check (ok).
+__device__ __forceinline__ double fk_error_cs(const double *jc, const double c[4],
+                                              const double s[4], bool ok, double px, double py,
+                                              double pz) {
   double x = jc[12], y = 0.0, z = jc[13];  // B4 e4 = (a4, 0, d4)
 #pragma unroll
   for (int i = 3; i >= 0; --i) {
-    ok = ok && angle_ok(th[i]);
-    double s, c;
-    sincos_fk(th[i], &s, &c);  // |th| <= 2 pi here (ok); outside, the result is NaN anyway
-    double xr = c * x - s * y, yr = s * x + c * y;  // Rz(t_i)
+    double xr = c[i] * x - s[i] * y, yr = s[i] * x + c[i] * y;  // Rz(t_i)
     x = xr;
     y = yr;
     if (i > 0) {  // B_{i} (1-based), i.e. jc[i - 1]
@@ -369,6 +356,18 @@ __device__ __forceinline__ double fk_error(const double *jc, const double th[4],
   }
   d3 e = {x, y, z}, p = {px, py, pz};
   return ok ? dist3(e, p) : __builtin_nan("");
+}
+
+__device__ __forceinline__ double fk_error(const double *jc, const double th[4], double px,
+                                           double py, double pz, int alpha_bad) {
+  bool ok = !alpha_bad;
+  double c[4], s[4];
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    ok = ok && angle_ok(th[i]);
+    sincos_fk(th[i], &s[i], &c[i]);  // |th| <= 2 pi here (ok); outside, the result is NaN anyway
+  }
+  return fk_error_cs(jc, c, s, ok, px, py, pz);
 }
 
 // Same chain, writing all four cumulative transforms (row-major 4x4 each).
@@ -554,7 +553,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          double *fk_err, bool check_limits, void *scratch, DevStats *S, hipStream_t st,
                          int variant, int core, FabOrderDev *ord, const RobotConstDev *rc,
-                         unsigned long long *dbg, int bpc = 0);
+                         unsigned long long *dbg, int bpc = 0, bool prior = false);
 constexpr size_t kFabrikDebugWords = 64 + 24 * 4096;  // diagnostic build: totals + per-wave records
 // Per-robot seed constants (RobotConstDev) into device memory, on stream st.
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t st);

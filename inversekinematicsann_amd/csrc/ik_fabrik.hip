@@ -187,11 +187,31 @@ __device__ __forceinline__ double py_round8_core(double v, bool &ok) {
   return r;
 }
 
+// sqrt(1 - v^2) = sin(acos(v)) for |v| <= 1 (the FK round trip's sines): 1 - v^2
+// in one rounding (fma), its root from the hardware estimate and one coupled
+// Newton step -- a few ulps, far inside the round trip's 1e-12 (its value is only
+// reported, never compared: tests/test_gpu_parity.py
+// ::test_fabrik_fk_err_equals_standalone_fk).
+__device__ __forceinline__ double sin_of_acos(double v) {
+  const double t = __builtin_fma(-v, v, 1.0);
+  const double y = __builtin_amdgcn_rsq(t);
+  const double h = 0.5 * y, g = t * y;
+  const double e = __builtin_fma(-h, g, 0.5);
+  return t > 0.0 ? __builtin_fma(g, e, g) : 0.0;
+}
+
 // __get_angles (inverse.py:54-112) through the core sequences; returns false
 // (and the caller runs get_angles) when some radicand or quotient leaves their
 // domains -- coincident joints, a zero divisor, non-finite joints -- or the
 // effector's x or y is zero or extreme (atan2's special cases).
-__device__ __forceinline__ bool get_angles_core(const d3 J[4], double th[4], int &st) {
+// cs / sn: the angles' cosines and sines for the FK round trip (cli.py:54-61),
+// from the values the angles come from instead of sin / cos of the angles:
+// theta_1 = atan2(E.y, E.x) gives (E.x, E.y) / |(E.x, E.y)|, and every other angle
+// is +-(k pi / 2 -+ acos(v)) of a law-of-cosines value v, so its cosine and sine
+// are +-v and +-sqrt(1 - v^2).  They differ from sin / cos of the rounded angles
+// by a few ulps (the rounding of the angles themselves), not 4 x 40 instructions.
+__device__ __forceinline__ bool get_angles_core(const d3 J[4], double th[4], int &st,
+                                                double cs[4], double sn[4]) {
   const d3 A = {0.0, 0.0, 0.0};
   const d3 B = J[0], C = J[1], D = J[2], E = J[3];
   uint32_t dom = 0;
@@ -209,31 +229,54 @@ __device__ __forceinline__ bool get_angles_core(const d3 J[4], double th[4], int
   };
   double num = (sq(ab) + sq(bc)) - sq(ac);
   double den = 2 * ab * bc;
-  const double a2 = acos_py(py_round8_core(quot(num, den), ok));
-  th[1] = (C.x * D.x < 0) ? ((3 * kPi / 2) - a2) : -(kPi / 2 - a2);
+  const double v2 = py_round8_core(quot(num, den), ok);
+  const double a2 = acos_py(v2);
+  const bool up = C.x * D.x < 0;
+  th[1] = up ? ((3 * kPi / 2) - a2) : -(kPi / 2 - a2);
+  const double w2 = sin_of_acos(v2);
+  cs[1] = up ? -w2 : w2;  // cos(3 pi / 2 - a) = -sin a, cos(a - pi / 2) = sin a
+  sn[1] = -v2;            // sin of either is -cos a
   const double bd = dist3c(B, D, dom);
   num = (sq(bc) + sq(cd)) - sq(bd);
   den = 2 * bc * cd;
-  const double a3 = acos_py(py_round8_core(quot(num, den), ok));
+  const double v3 = py_round8_core(quot(num, den), ok);
+  const double a3 = acos_py(v3);
   th[2] = -(kPi - a3);
+  cs[2] = -v3;  // a - pi
+  sn[2] = -sin_of_acos(v3);
   const double ce = dist3c(C, E, dom);
   num = (sq(cd) + sq(de)) - sq(ce);
   den = 2 * cd * de;
-  const double a4 = acos_py(py_round8_core(quot(num, den), ok));
+  const double v4 = py_round8_core(quot(num, den), ok);
+  const double a4 = acos_py(v4);
   // get_point_between(C, E, |C - E| / 2): |C - E| is ce again (the radicand squares
   // E - C = -(C - E) exactly) and (ce / 2) / ce is exactly 0.5 for a ce in the domain
   const d3 m = {C.x + (0.5 * (E.x - C.x)), C.y + (0.5 * (E.y - C.y)), C.z + (0.5 * (E.z - C.z))};
   const double da = dist3c(B, m, dom);
   th[3] = (bd > da) ? -(kPi - a4) : (kPi - a4);  // db = |B - D| = bd
-  // th[0] = atan2_fast(E.y, E.x): by the caller, after the fallback pass
+  cs[3] = -v4;  // a - pi or pi - a
+  const double w4 = sin_of_acos(v4);
+  sn[3] = (bd > da) ? -w4 : w4;
+  // th[0] = atan2_fast(E.y, E.x): by the caller, after the fallback pass; its
+  // cosine and sine from E (E.x, E.y in the division domain: t is normal)
+  {
+    const double t = E.x * E.x + E.y * E.y;
+    const double y = __builtin_amdgcn_rsq(t);
+    const double h = 0.5 * y, g = t * y;
+    const double e = __builtin_fma(-h, g, 0.5);
+    const double yi = __builtin_fma(y, e, y);
+    cs[0] = E.x * yi;
+    sn[0] = E.y * yi;
+  }
   return ok && dom < kCoreDom;
 }
 
 // Seed pose, inverse.py:123-130: FK of [atan2(y, x), thetas[1:]] (the
-// reference writes theta_1 into dh_matrix[0][0] and runs fkine on that row),
-// through the per-robot constants (seed_chain; same bits as fk_chain).
+// reference writes theta_1 into dh_matrix[0][0] and runs fkine on that row), in
+// closed form from the per-robot constants (seed_closed, ik_common.h; r05 and
+// before: seed_chain, the DH chain's own products).
 __device__ __forceinline__ int seed_pose(const RobotConstDev *rc, d3 g, d3 J[4]) {
-  return seed_chain(rc, atan2(g.y, g.x), J);
+  return seed_closed(rc, g, J);
 }
 
 // The per-robot constants (RobotConstDev).  jc / alpha_bad come from the host
@@ -246,21 +289,25 @@ struct FkTrip {
 __global__ void robot_const_kernel(RobotDev r, FkTrip t, RobotConstDev *rc) {
   if (threadIdx.x != 0) return;
   int st = IK_OK;
-  for (int k = 1; k < 4; ++k) {
-    dh_transform(r.dh[k], r.dh[4 + k], r.dh[8 + k], r.dh[12 + k], rc->A[k - 1]);
+  for (int k = 1; k < 4; ++k)
     if (!angle_ok(r.dh[k])) st = IK_E_ANGLE_RANGE;
-  }
   for (int k = 0; k < 4; ++k)
     if (!angle_ok(r.dh[12 + k])) st = IK_E_ANGLE_RANGE;
-  const double al = r.dh[12];
-  rc->ca1 = cos(al);
-  rc->sa1 = sin(al);
-  rc->d1 = r.dh[4];
-  rc->a1 = r.dh[8];
   for (int k = 0; k < 6; ++k) rc->lim[k] = r.lim[k];
   for (int k = 0; k < 16; ++k) rc->jc[k] = t.jc[k];
   rc->alpha_bad = t.alpha_bad;
   rc->st = st;
+  // seed_closed's P_k: the seed chain at theta_1 = 0 (Rz(0) = I exactly)
+  {
+    const double th[4] = {0.0, r.dh[1], r.dh[2], r.dh[3]};
+    d3 P[4];
+    (void)fk_chain(r.dh, th, P);
+    for (int j = 0; j < 4; ++j) {
+      rc->P[j][0] = P[j].x;
+      rc->P[j][1] = P[j].y;
+      rc->P[j][2] = P[j].z;
+    }
+  }
 }
 
 void launch_robot_const(const RobotDev &r, RobotConstDev *rc, hipStream_t stream) {
@@ -310,6 +357,7 @@ struct FabArgs {
   int32_t *perm;    // queue position -> point index
   uint16_t *cell;   // per point: goal cell (bits 0-9) | cost class << 10
   FabOrderDev *ord; // context-owned cost table
+  int prior_gate;   // the table is a built-in prior no call has taught yet (see scatter)
   unsigned long long *dbg;  // diagnostic build only: iteration-kernel counters
 };
 
@@ -325,6 +373,15 @@ enum { kDiagTStart = kDiagCount, kDiagTDry, kDiagTLast, kDiagStepsDry, kDiagTDra
        kDiagTRefill, kDiagTSub, kDiagDrainN, kDiagTDrain2, kDiagHwId, kDiagWords = 24 };
 #ifdef IKHIP_DIAG
 constexpr int kDiagWaveMax = 4096;  // = (kFabrikDebugWords - 64) / kDiagWords (24)
+#endif
+
+// Phase marks for the instruction census (tools/isa_phases.py): an analysis build
+// with -DIKHIP_PHASE_MARKS puts an assembly comment at each phase boundary of the
+// iteration kernel; the production build has none.
+#ifdef IKHIP_PHASE_MARKS
+#define IKHIP_MARK(s) asm volatile(";@phase " s)
+#else
+#define IKHIP_MARK(s) ((void)0)
 #endif
 
 static int env_int(const char *name, int dflt) {
@@ -359,7 +416,9 @@ __device__ __forceinline__ bool outside_rc(RcConst k, d3 g) {
 // angles, iterations, joints, the FK round trip (cli.py:54-61) and the per-lane
 // sums of the batch stats.
 __device__ __forceinline__ void commit_point(const FabArgs &a, int64_t i, const d3 J[4], d3 g,
-                                             int it, int st, const double th[4], LaneAcc &acc) {
+                                             int it, int st, const double th[4],
+                                             const double cs[4], const double sn[4],
+                                             LaneAcc &acc) {
   if (st != IK_OK) record_error(a.S, i, st);
   double2 *o = reinterpret_cast<double2 *>(a.ang + 4 * i);
   o[0] = make_double2(th[0], th[1]);
@@ -371,13 +430,19 @@ __device__ __forceinline__ void commit_point(const FabArgs &a, int64_t i, const 
   acc.max_it = max(acc.max_it, it);
   if (a.fk_err) {
     double e = __builtin_nan("");
+    IKHIP_MARK("commit.fk");
     if (st == IK_OK) {
       const RcConst k = opaque_rc(a.rc);
       double jc[16];
 #pragma unroll
       for (int e2 = 0; e2 < 16; ++e2) jc[e2] = k->jc[e2];
-      e = fk_error(jc, th, g.x, g.y, g.z, k->alpha_bad);
+      // (the angles' own range, forward.py:23-25: always within 2 pi here)
+      bool ok = !k->alpha_bad;
+#pragma unroll
+      for (int e2 = 0; e2 < 4; ++e2) ok = ok && angle_ok(th[e2]);
+      e = fk_error_cs(jc, cs, sn, ok, g.x, g.y, g.z);
     }
+    IKHIP_MARK("commit.fk_end");
     a.fk_err[i] = e;
     if (e == e) {
       acc.fk_max = fmax(acc.fk_max, e);
@@ -392,32 +457,38 @@ __device__ __forceinline__ void commit_point(const FabArgs &a, int64_t i, const 
 // a pass of its own, so the general code's registers are never live beside the
 // fast path's.  has: the lane holds a point; st: its status so far.
 template <class Joints>
-__device__ __forceinline__ void angles_step(bool has, Joints joints, int &st, double th[4]) {
+__device__ __forceinline__ void angles_step(bool has, Joints joints, int &st, double th[4],
+                                            double cs[4], double sn[4]) {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) th[k] = __builtin_nan("");
+  for (int k = 0; k < 4; ++k) th[k] = cs[k] = sn[k] = __builtin_nan("");
   bool redo = false, fast = false;
   if (has && st == IK_OK) {
     d3 J[4];
     joints(J);
     int sf = IK_OK;
-    fast = get_angles_core(J, th, sf);
+    fast = get_angles_core(J, th, sf, cs, sn);
     redo = !fast;
     if (fast) st = sf;
   }
+  IKHIP_MARK("angles.general");
   if (__any(redo)) {  // wave-uniform and rare: coincident joints, zero divisors, x = 0 or y = 0
     if (redo) {
       d3 J[4];
       joints(J);
       get_angles(J, th, st);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sincos_fk(th[k], &sn[k], &cs[k]);
     }
   }
   // theta_1 (inverse.py:60) last: kept out of the fast pass, whose registers
   // then fit beside the general pass's without spilling
+  IKHIP_MARK("angles.atan2");
   if (fast) {
     d3 J[4];
     joints(J);
     th[0] = atan2_fast(J[3].y, J[3].x);
   }
+  IKHIP_MARK("angles.end");
 }
 
 // ------------------------------------------------------------- simple ----
@@ -443,12 +514,12 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
       }
     }
   }
-  double th[4];
+  double th[4], cs[4], sn[4];
   angles_step(i < a.n, [&](d3 *o) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) o[k] = J[k];
-  }, st, th);
-  if (i < a.n) commit_point(a, i, J, g, it, st, th, acc);
+  }, st, th, cs, sn);
+  if (i < a.n) commit_point(a, i, J, g, it, st, th, cs, sn, acc);
   block_iter_stats_acc(a.S, acc.sum_it, acc.capped, acc.max_it);
   if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
 }
@@ -549,8 +620,8 @@ __device__ void order_fold(FabOrderDev *T, unsigned int ns) {
 // address per class took ~1k same-address atomics per launch at 1M points).
 // The cell -> class map of this call is built in LDS first.
 __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
-  __shared__ unsigned int cnt[kOrdClasses];
-  __shared__ uint8_t cls[kOrdCells];
+  __shared__ unsigned int cnt[kOrdClasses], unseen;
+  __shared__ uint8_t cls[kOrdCells];  // the cell's class, 0xff: unseen (the hardest class)
   const int t = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * (256 * kOrdPPT);
   d3 g[kOrdPPT];
@@ -560,6 +631,7 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
     if (i < a.n) g[j] = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
   }
   if (t < kOrdClasses) cnt[t] = 0;
+  if (t == 0) unseen = 0;
   // the cell -> class map's table reads, in flight with the goals'
   static_assert(kOrdCells % 256 == 0, "whole table rows per thread");
   unsigned int key[kOrdCells / 256];
@@ -567,21 +639,42 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
   for (int q = 0; q < kOrdCells / 256; ++q) key[q] = a.ord->key[t + 256 * q];
 #pragma unroll
   for (int q = 0; q < kOrdCells / 256; ++q)
-    cls[t + 256 * q] = (uint8_t)key_class(key[q], a.max_iter);
+    cls[t + 256 * q] = key[q] ? (uint8_t)key_class(key[q], a.max_iter) : (uint8_t)0xff;
   __syncthreads();
+  unsigned int nu = 0;
 #pragma unroll
   for (int j = 0; j < kOrdPPT; ++j) {
     const int64_t i = b0 + j * 256 + t;
     if (i < a.n) {
       const int cell = goal_cell(a.r, g[j]);
-      const int k = cls[cell];
+      int k = cls[cell];
+      nu += k == 0xff ? 1u : 0u;
+      k = k == 0xff ? kOrdClasses - 1 : k;
       a.cell[i] = (uint16_t)(cell | (k << 10));
       atomicAdd(&cnt[k], 1u);
     }
   }
+  // (only the prior's gate reads the count: the first call of a context; a
+  // wave sum, then one LDS atomic per wave -- one per thread cost 2 us a launch)
+  if (a.prior_gate) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nu += __shfl_xor(nu, off, 64);
+    if ((t & 63) == 0 && nu) atomicAdd(&unseen, nu);
+  }
   __syncthreads();
   if (t < kOrdClasses && cnt[t]) atomicAdd(&a.S->cls_tot[t][blockIdx.x % kOrdShards], cnt[t]);
+  if (t == 0 && unseen) atomicAdd(&a.S->unseen, (unsigned long long)unseen);
 }
+
+// The built-in prior's gate: a table no call has taught yet is
+// the prior learned on random_dist batches (ik_fabrik_prior.h).  On a batch of
+// another distribution many goals fall in cells it has never seen (uniform box:
+// the unreachable far cells; a spring trajectory: the far end of its curve), and
+// ordering by it measured slower than point order (r06 lease: uniform box +1.5 %,
+// spring +2.3 %).  When more than 1 / kPriorUnseenDiv of the batch lands in unseen
+// cells, the first call keeps point order; the call's records then teach the
+// table as usual.
+constexpr unsigned kPriorUnseenDiv = 50;
 
 // 2. scatter: perm[queue position] = point.  The queue is class-major (hardest
 // first), then shard: region (c, s) starts after every harder class and every
@@ -590,6 +683,9 @@ __global__ __launch_bounds__(256) void fabrik_classify_kernel(FabArgs a) {
 // per class and hands the slots out through LDS atomics.
 __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
   static_assert(kOrdClasses * kOrdShards == 256, "one total per thread");
+  // the prior does not describe this batch (see above): every point in the last
+  // class, i.e. the order an empty table gives (block shards, point order inside)
+  const bool gated = a.prior_gate && a.S->unseen * kPriorUnseenDiv > (unsigned long long)a.n;
   __shared__ unsigned int cnt[kOrdClasses], base[kOrdClasses];
   __shared__ unsigned int tot[kOrdClasses][kOrdShards], ctot[kOrdClasses];
   const int t = threadIdx.x;
@@ -603,8 +699,18 @@ __global__ __launch_bounds__(256) void fabrik_scatter_kernel(FabArgs a) {
   for (int j = 0; j < kOrdPPT; ++j) {
     const int64_t i = b0 + j * 256 + t;
     cl[j] = i < a.n ? a.cell[i] : (uint16_t)0xffff;
+    if (gated && cl[j] != 0xffff) cl[j] |= (uint16_t)((kOrdClasses - 1) << 10);
   }
   __syncthreads();
+  if (gated) {  // (uniform) the shards' totals all in the last class
+    unsigned int col = 0;
+    if (t < kOrdShards)
+      for (int c = 0; c < kOrdClasses; ++c) col += tot[c][t];
+    __syncthreads();
+    if (t < kOrdShards)
+      for (int c = 0; c < kOrdClasses; ++c) tot[c][t] = c == kOrdClasses - 1 ? col : 0u;
+    __syncthreads();
+  }
 #pragma unroll
   for (int j = 0; j < kOrdPPT; ++j)
     if (cl[j] != 0xffff) atomicAdd(&cnt[cl[j] >> 10], 1u);
@@ -701,6 +807,7 @@ template <bool ORD>
 __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int cnt, int lane,
                                            LaneAcc &acc) {
   prio_raise();
+  IKHIP_MARK("flush.angles");
   __builtin_amdgcn_wave_barrier();
   const bool has = lane < cnt;
   // the joints from the ring each time they are needed (LDS reads are cheap; the
@@ -712,15 +819,16 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
   const double2 meta = R.w[lane][8];
   const uint64_t itst = (uint64_t)__double_as_longlong(meta.y);
   int st = has ? (int)(itst >> 32) : IK_OK;
-  double th[4];
-  angles_step(has, joints, st, th);
+  double th[4], cs[4], sn[4];
+  angles_step(has, joints, st, th, cs, sn);
+  IKHIP_MARK("flush.commit");
   if (has) {
     d3 J[4];
     joints(J);
     const int64_t i = __double_as_longlong(meta.x);
     const int it = (int)(uint32_t)itst;
     const double2 g01 = R.w[lane][6], g2 = R.w[lane][7];
-    commit_point(a, i, J, {g01.x, g01.y, g2.x}, it, st, th, acc);
+    commit_point(a, i, J, {g01.x, g01.y, g2.x}, it, st, th, cs, sn, acc);
     if constexpr (ORD) {
       if (i % kOrdSample == 0 && i / kOrdSample < kOrdMaxSample) {
         const uint32_t lo = (uint32_t)(it < 0xffff ? it : 0xffff);
@@ -728,6 +836,7 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
       }
     }
   }
+  IKHIP_MARK("flush.end");
   __builtin_amdgcn_wave_barrier();
   prio_drop();
 }
@@ -773,9 +882,14 @@ fabrik_iter_kernel(FabArgs a) {
 
   // prepared points: the batch's entry j in slot j of the wave's LDS batch
   // (wave-uniform count / cursor); a refilled lane reads its entry from there
-  struct PrepBatch {  // per entry seven 16-byte words: seed joints 0..2, goal, index
+  struct PrepBatch {  // per entry seven 16-byte words: seed joints 0..2, goal, {meta, cq}
     double2 w[64][7];
   };
+  // an entry's meta word: the point index, and (CORE 2) whether the seed's carried
+  // radicand is outside the core domain (bit 62) and whether the launch's error
+  // band covers the point (bit 61) -- the carry itself (reuse_carry) and the band
+  // test are taken at full width in the preparation, not per refill (r06)
+  constexpr uint64_t kMetaCdomBad = 1ull << 62, kMetaBok = 1ull << 61;
   __shared__ PrepBatch batches[4];
   PrepBatch &PB = batches[threadIdx.x >> 6];
   int pcount = 0, pptr = 0;
@@ -857,6 +971,7 @@ fabrik_iter_kernel(FabArgs a) {
     IKHIP_DG(kDiagLoops, 1);
     if (!dry && (nfree >= REFILL_MIN || nfree == 64)) {
       prio_raise();
+      IKHIP_MARK("refill.park");
       IKHIP_DG(kDiagRefills, 1);
       IKHIP_DT(kDiagTRefill);  // refill time, less the flushes and preparations in it
       IKHIP_DT(kDiagTSub);
@@ -882,6 +997,7 @@ fabrik_iter_kernel(FabArgs a) {
       }
       IKHIP_DT_ACC(kDiagParkTicks, kDiagTSub);
       IKHIP_DT(kDiagTSub);
+      IKHIP_MARK("refill.handout");
       // the next batch's three stages (called below: one per refill ahead of time,
       // or back to back just before a preparation)
       auto stage1 = [&]() {
@@ -946,7 +1062,16 @@ fabrik_iter_kernel(FabArgs a) {
         J1 = {w1.y, w2.x, w2.y};
         J2 = {w3.x, w3.y, w4.x};
         g = {w4.y, w5.x, w5.y};
-        out = __double_as_longlong(w[6].x);
+        const double2 w6 = w[6];
+        const uint64_t meta = (uint64_t)__double_as_longlong(w6.x);
+        out = (int64_t)(meta & (kMetaBok - 1));
+        if constexpr (CORE == 2) {
+          // the seed's carry (reuse_carry): cd = goal - J2, exact, as it computes it
+          cq = w6.y;
+          cd = {g.x - J2.x, g.y - J2.y, g.z - J2.z};
+          cdom = (meta & kMetaCdomBad) ? 0xffffffffu : 0u;
+          bok = (meta & kMetaBok) != 0;
+        }
       };
       // (read before a preparation overwrites the batch)
       if (mine) take_entry(pptr + rank);
@@ -958,6 +1083,7 @@ fabrik_iter_kernel(FabArgs a) {
       // lanes stay free, the inner loop returns at once and the next refill goes on.
       // (diagnostic build: before a preparation the stages count as preparation time,
       // as the r04 / r05 breakdowns did, so that staging is the lookahead's cost)
+      IKHIP_MARK("refill.stages");
       if (prep) IKHIP_DT(kDiagTDrain);  // (scratch slot: the preparation's start)
       bool more = true;
       if (nstage == 0 && (prep || avail <= 24)) { stage1(); more = prep; }
@@ -970,12 +1096,24 @@ fabrik_iter_kernel(FabArgs a) {
         pcount = ncount;
         nstage = 0;
         prio_raise();
+        IKHIP_MARK("refill.prepare");
         if (lane < pcount) {
           const RcConst k = opaque_rc(a.rc);
           if (a.check_limits && outside_rc(k, ng))
             atomicMin(&a.S->first_oob, (unsigned long long)ni);
           d3 Js[4];
           (void)seed_pose((const RobotConstDev *)k, ng, Js);
+          uint64_t meta = (uint64_t)ni;
+          double pcq = 0.0;
+          if constexpr (CORE == 2) {
+            d3 pcd;
+            uint32_t pcdom;
+            reuse_carry(Js[2], ng, L[3], pcq, pcd, pcdom);
+            const bool pbok = fabs(Js[0].x) + fabs(Js[0].y) + fabs(Js[0].z) + fabs(ng.x) +
+                                  fabs(ng.y) + fabs(ng.z) <=
+                              a.band_n1;
+            meta |= (pcdom < kCoreDom ? 0ull : kMetaCdomBad) | (pbok ? kMetaBok : 0ull);
+          }
           double2 *w = PB.w[lane];
           w[0] = {Js[0].x, Js[0].y};
           w[1] = {Js[0].z, Js[1].x};
@@ -983,7 +1121,7 @@ fabrik_iter_kernel(FabArgs a) {
           w[3] = {Js[2].x, Js[2].y};
           w[4] = {Js[2].z, ng.x};
           w[5] = {ng.y, ng.z};
-          w[6] = {__longlong_as_double(ni), 0.0};
+          w[6] = {__longlong_as_double((long long)meta), pcq};
         }
 #ifdef IKHIP_DIAG
         // (the seed's loads are consumed before the stamp)
@@ -993,6 +1131,7 @@ fabrik_iter_kernel(FabArgs a) {
         IKHIP_DT_ACC(kDiagTRefill, kDiagTDrain);  // (not refill time)
         // the rest of the free lanes from the new batch (a short last chunk may leave
         // some free until the next refill)
+        IKHIP_MARK("refill.handout2");
         const int take2 = min(nfree - take1, pcount);
         const bool mine2 = wasfree && rank >= take1 && rank < take1 + take2;
         __builtin_amdgcn_wave_barrier();  // the batch's LDS writes before the reads
@@ -1000,17 +1139,15 @@ fabrik_iter_kernel(FabArgs a) {
         pptr = take2;
         mine = mine || mine2;
       }
+      IKHIP_MARK("refill.start");
       if (mine) {
         st = IK_OK;
         cont = true;  // the loop's initial errors of 1.0 (fabrik.py:53-54) exceed tol
         step = 0;
         active = true;
-        if constexpr (CORE == 2) {
-          reuse_carry(J2, g, L[3], cq, cd, cdom);
-          bok = fabs(J0.x) + fabs(J0.y) + fabs(J0.z) + fabs(g.x) + fabs(g.y) + fabs(g.z) <=
-                a.band_n1;
-        }
+        // (CORE 2: the carry and the band flag came with the entry, take_entry)
       }
+      IKHIP_MARK("refill.end");
       dry = nstage < 0 && pptr >= pcount;
       IKHIP_DT_ACC(kDiagRefillTicks, kDiagTRefill);
       // a dry wave's last lanes are the launch's tail: they iterate at priority 1,
@@ -1024,7 +1161,12 @@ fabrik_iter_kernel(FabArgs a) {
     // iterate until a refill is due (REFILL_MIN lanes free) or, once the queue is
     // dry, until every lane has stopped: the refill's scalar state stays out of
     // this loop, so its SGPRs are not reloaded from their spill lanes per iteration
+    IKHIP_MARK("loop");
     const int need = __builtin_amdgcn_readfirstlane(dry ? 64 : REFILL_MIN);  // (an SGPR)
+    // (r06: the loop's control as uint64 wave masks instead of these lane bools
+    // measured worse in the ISA: the masks, updated inside the divergent step,
+    // went to VGPRs and took ~25 VALU per iteration; the bools live in SGPR lane
+    // masks already, and only ballot(!run) costs a v_cndmask + v_cmp)
     while (true) {
 #ifdef IKHIP_DIAG
     {
@@ -1092,6 +1234,7 @@ fabrik_iter_kernel(FabArgs a) {
     }
   }
   // drain: park the last finished lanes, then the angles step on the ring
+  IKHIP_MARK("drain");
   IKHIP_DT(kDiagTDrain);
   {
     const unsigned long long pm = __ballot(pending);
@@ -1180,7 +1323,8 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
                          int max_iter, double *ang, int32_t *iters, double *joints,
                          double *fk_err, bool check_limits, void *scratch, DevStats *S,
                          hipStream_t stream, int variant, int core_req, FabOrderDev *ord,
-                         const RobotConstDev *rc, unsigned long long *dbg, int bpc_req) {
+                         const RobotConstDev *rc, unsigned long long *dbg, int bpc_req,
+                         bool prior) {
   if (n <= 0) return;
   FabArgs a;
   a.r = r;
@@ -1209,6 +1353,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
   a.perm = nullptr;
   a.cell = nullptr;
   a.ord = ord;
+  a.prior_gate = prior ? 1 : 0;
   // the seed's own angles (robot_const_kernel's check, forward.py:23-25)
   bool robot_ok = true;
   for (int k = 1; k < 4; ++k)

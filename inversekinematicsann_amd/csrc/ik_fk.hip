@@ -14,7 +14,7 @@ __global__ void reset_stats_kernel(DevStats *S) {
   if (t == 0) {
     S->first_oob = ~0ull;
     S->first_err_key = ~0ull;
-    S->ticket = 0;
+    S->unseen = 0;
   }
   if (t < kQueueHeads) S->heads[t][0] = 0;
   for (int e = t; e < kOrdClasses * kOrdShards; e += blockDim.x) {

@@ -68,21 +68,44 @@ def test_fabrik_vs_oracle_random(ctx):
         assert np.abs(jo - rjo).max() <= 1e-9
 
 
-def test_fabrik_tol_zero_and_negative(ctx):
+def test_fabrik_tol_zero_and_negative():
     """tol = 0 (and tols whose threshold rounds to 0, or below it) is accepted by
-    the reference (fabrik.py:57: the loop stops only when both errors are exactly
-    0).  The kernels' error band must then decide nothing: a lane whose b0 lands
-    exactly on start (se2 == 0) while |1 - q| sqrt(x) > 0 stops with the reference
-    (ADVICE r05).  ~12 % of these points stop before the cap at tol 0."""
+    the reference (fabrik.py:57: the loop then stops only where both errors are
+    exactly 0, i.e. on an exact fixed point of the chain).  The kernels' error
+    band must decide nothing there: the band-deciding kernel (split,
+    CORE 2) gives the same iteration counts and the same bits as the kernel that
+    compares every error exactly (simple), on every point.  Against the oracle the
+    counts cannot be bit-exact at tol 0 alone: whether a chain lands on an exact
+    fixed point depends on every bit of its trajectory, and the seed's cos / sin /
+    atan2 (ocml) may differ from glibc's in the last ulp; so there
+    the angles are checked (<= 1e-9) and the points whose counts differ must be
+    few and must have converged in one of the two runs."""
+    from inversekinematicsann_amd import _native
     from inversekinematicsann_amd.robot.position_generator import random_dist
     pts = random_dist(20_000, seed=11)
-    for tol, mi in ((0.0, 100), (1e-300, 100), (-1.0, 5)):
-        ang, it, jo, st = ctx.fabrik_solve(pts, tol, mi, want_joints=True)
-        rang, rit, rjo, rst = O.fabrik_ikine(pts, tol, mi)
-        assert np.array_equal(it, rit), (tol, int((it != rit).sum()))
-        assert np.abs(ang - rang).max() <= 1e-9, tol
-        assert np.abs(jo - rjo).max() <= 1e-9, tol
-    assert int((rit < 5).sum()) == 0
+    ctxs = {}
+    try:
+        for name, v in (("simple", 0), ("split", 1)):
+            os.environ["IKHIP_FABRIK_VARIANT"] = str(v)
+            ctxs[name] = _native.Context(0)
+        os.environ.pop("IKHIP_FABRIK_VARIANT", None)
+        for tol, mi in ((0.0, 100), (1e-300, 100), (-1.0, 5)):
+            out = {k: c.fabrik_solve(pts, tol, mi, want_joints=True) for k, c in ctxs.items()}
+            (a0, i0, j0, _), (a1, i1, j1, _) = out["simple"], out["split"]
+            assert np.array_equal(i0, i1), (tol, int((i0 != i1).sum()))
+            assert np.array_equal(a0, a1, equal_nan=True) and np.array_equal(j0, j1)
+            rang, rit, rjo, rst = O.fabrik_ikine(pts, tol, mi)
+            assert np.abs(a1 - rang).max() <= 1e-9, tol
+            assert np.abs(j1 - rjo).max() <= 1e-9, tol
+            bad = i1 != rit
+            assert bad.sum() <= 0.01 * len(pts), (tol, int(bad.sum()))
+            assert ((i1[bad] < mi) | (rit[bad] < mi)).all(), tol
+            if tol < 0:
+                assert (i1 == mi).all() and (rit == mi).all()
+    finally:
+        os.environ.pop("IKHIP_FABRIK_VARIANT", None)
+        for c in ctxs.values():
+            c.close()
 
 
 def test_fabrik_ragged_sizes(ctx):
@@ -609,6 +632,35 @@ def test_fabrik_work_order_is_invisible():
         assert np.abs(first[0][:8192] - ref_ang).max() <= 1e-9
     finally:
         c.close()
+
+
+def test_fabrik_prior_gate_first_call_other_distributions():
+    """a fresh context's first call on a batch the built-in table
+    was not learned on (uniform workspace box, a spring trajectory; most goals in
+    cells the prior has never seen) keeps the empty table's order (the scatter's
+    gate, ik_fabrik.hip) -- and, gated or not, the results are the oracle's bit for
+    bit in the counts, identical to an empty-table solve, and the call teaches
+    the table as usual."""
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd.robot.position_generator import random_dist, spring
+    rng = np.random.default_rng(5)
+    box = np.stack([rng.uniform(0, 6, 40_000), rng.uniform(-6, 6, 40_000),
+                    rng.uniform(-3, 6, 40_000)], axis=1)
+    for pts in (box, spring(40_000, 2, 3, 6), random_dist(40_000, seed=6)):
+        c = _native.Context(0)
+        try:
+            prior = c.fabrik_order_get().copy()
+            ang, it, _, _ = c.fabrik_solve(pts, 1e-3, 100)
+            assert not np.array_equal(c.fabrik_order_get(), prior)  # learned
+            c.fabrik_order_set(None)
+            ang2, it2, _, _ = c.fabrik_solve(pts, 1e-3, 100)
+            assert np.array_equal(it, it2) and np.array_equal(ang, ang2, equal_nan=True)
+            rang, rit, _, _ = O.fabrik_ikine(pts[:8192], 1e-3, 100)
+            assert np.array_equal(it[:8192], rit)
+            assert np.array_equal(np.isnan(ang[:8192]), np.isnan(rang))
+            assert np.nanmax(np.abs(ang[:8192] - rang)) <= 1e-9
+        finally:
+            c.close()
 
 
 def test_fabrik_builtin_work_order_table():

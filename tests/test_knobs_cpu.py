@@ -12,7 +12,7 @@ from tests.conftest import ROOT
 CSRC = os.path.join(ROOT, "inversekinematicsann_amd", "csrc")
 # build-wide switches that are not tuning knobs: the diagnostic build and the two
 # translation units that re-include ik_ann.hip
-NOT_KNOBS = {"IKHIP_DIAG", "IKHIP_ANN_WIDE", "IKHIP_ANN_X_TU"}
+NOT_KNOBS = {"IKHIP_DIAG", "IKHIP_ANN_WIDE", "IKHIP_ANN_X_TU", "IKHIP_PHASE_MARKS"}
 DELETED = {"IKHIP_EXP_L1W", "IKHIP_FAB_FUSED_SCATTER", "IKHIP_FAB_PREP_CARRY", "IKHIP_ANN_CLAIM",
            "IKHIP_ANN_H16", "IKHIP_ANN_X16", "IKHIP_ANN_DYN", "IKHIP_ANN_HSWZ",
            "IKHIP_ANN_BIAS_FIRST", "IKHIP_ANN_H16_PATTERN", "IKHIP_ANN_X16_PATTERN",
@@ -61,6 +61,6 @@ def test_no_dropped_alternative_left():
     # diagnostic macro or an environment variable documented in INTEGRATION.md
     doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
     for name in sorted(used - NOT_KNOBS - set(source_knobs())):
-        if name in ("IKHIP_DG", "IKHIP_DT", "IKHIP_DT_ACC"):  # the diagnostic build's stamps
+        if name in ("IKHIP_DG", "IKHIP_DT", "IKHIP_DT_ACC", "IKHIP_MARK"):  # diagnostic / census builds
             continue
         assert f"`{name}`" in doc, name
