@@ -120,8 +120,8 @@ def parse(argv=None):
                     help="FABRIK: also time cold calls (work order forgotten); 0 for profiling "
                          "runs, whose per-kernel averages they would mix in")
     ap.add_argument("--traffic-file",
-                    default=os.path.join(ROOT, "profiles", "r05", "traffic.json"))
-    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r05", "pmc"),
+                    default=os.path.join(ROOT, "profiles", "r06", "traffic.json"))
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "r06", "pmc"),
                     help="committed PMC diagnosis summaries (pipe occupancy in the roofline)")
     ap.add_argument("--gather", type=int, default=1,
                     help="N>1: the sharded solve with the library's RCCL all-gather of every "

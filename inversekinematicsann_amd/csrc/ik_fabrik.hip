@@ -524,6 +524,29 @@ __global__ __launch_bounds__(256) void fabrik_simple_kernel(FabArgs a) {
   if (a.fk_err) wave_fk_stats(a.S, acc.fk_max, acc.fk_sum);
 }
 
+// The whole FABRIK solve of one goal in the general arithmetic (the simple
+// kernel's loop: fabrik.py:44-67 from the seed pose, inverse.py:123-133): the
+// iteration kernel's retire step re-solves the rare lanes whose core sequences
+// left their domain (kStRedo) with it.
+__device__ __forceinline__ void solve_general(const FabArgs &a, d3 g, d3 J[4], int &it,
+                                              int &st) {
+  st = seed_pose(a.rc, g, J);
+  it = 0;
+  double se = 1.0, ge = 1.0;
+  if (st != IK_OK) return;
+  while (((se > a.tol2) || (ge > a.tol2)) && (a.max_iter > it)) {
+    fabrik_step4(J[0], J[1], J[2], J[3], g, a.r.links, se, ge, st);
+    ++it;
+    if (st != IK_OK) break;
+  }
+}
+// A lane of the iteration kernel whose core sequences left their domain
+// (coincident joints, non-finite or extreme coordinates: sqrt_core / div_core
+// would not give the general sequences' bits) stops with this status; the retire
+// step re-solves its goal with solve_general (r06: no copy of the pre-step state
+// is kept for an in-loop redo).
+constexpr int kStRedo = 0x40;
+
 // ---------------------------------------------------------- Work order ----
 // The persistent iteration kernel hands points out in queue order.  In point
 // order a 100-iteration point can be picked up just before the queue runs dry
@@ -816,9 +839,21 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
     asm volatile("" ::: "memory");
     ring_joints(R, lane, J);
   };
-  const double2 meta = R.w[lane][8];
-  const uint64_t itst = (uint64_t)__double_as_longlong(meta.y);
+  double2 meta = R.w[lane][8];
+  uint64_t itst = (uint64_t)__double_as_longlong(meta.y);
   int st = has ? (int)(itst >> 32) : IK_OK;
+  if (__builtin_expect(__any(has && st == kStRedo), 0)) {  // wave-uniform, rare
+    if (has && st == kStRedo) {
+      const double2 g01 = R.w[lane][6], g2 = R.w[lane][7];
+      d3 J[4];
+      int it2;
+      solve_general(a, {g01.x, g01.y, g2.x}, J, it2, st);
+      ring_put(R, lane, J[0], J[1], J[2], J[3], {g01.x, g01.y, g2.x},
+               __double_as_longlong(meta.x), it2, st);
+      itst = ((uint64_t)(uint32_t)st << 32) | (uint32_t)it2;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
   double th[4], cs[4], sn[4];
   angles_step(has, joints, st, th, cs, sn);
   IKHIP_MARK("flush.commit");
@@ -1190,24 +1225,13 @@ fabrik_iter_kernel(FabArgs a) {
       if (__popcll(__builtin_amdgcn_ballot_w64(!run)) >= need) break;  // (a bool: no VGPR round trip)
       if (run) {
         if constexpr (CORE == 2) {
-          uint32_t dom = 0, cdom_n = cdom;
-          d3 n1 = J1, n2 = J2, cd_n = cd;
-          double cq_n = cq;
-          bool cont_n;
-          fabrik_step4_lazy(J0, n1, n2, g, L, a.band, bok, tol2, cont_n, cq_n, cd_n, cdom_n, dom);
-          if (__all(dom < kCoreDom)) {
-            J1 = n1; J2 = n2;
-            cq = cq_n;
-            cd = cd_n;
-            cdom = cdom_n;
-            cont = cont_n;
-          } else {
-            IKHIP_DG(kDiagFallbacks, 1);
-            double se, ge;
-            fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
-            reuse_carry(J2, g, L[3], cq, cd, cdom);
-            cont = (se > tol2) || (ge > tol2g);
-          }
+          // in place: a lane whose radicands leave the core domain stops with
+          // kStRedo and the retire step re-solves it in the general arithmetic
+          // (solve_general), so no copy of the pre-step state is kept (r06: the
+          // wave-wide in-loop redo needed one, 7 register moves per iteration)
+          uint32_t dom = 0;
+          fabrik_step4_lazy(J0, J1, J2, g, L, a.band, bok, tol2, cont, cq, cd, cdom, dom);
+          if (dom >= kCoreDom) st = kStRedo;
         } else if constexpr (CORE == 1) {
           // wave-uniform fallback: when any lane's radicand leaves sqrt_core's
           // domain (coincident joints, non-finite input) the wave redoes the
