@@ -640,14 +640,20 @@ def run_fabrik(job, args, tol=None, max_iter=None):
 FK_BYTES_PER_POINT = 32 + 24   # float64 angles in, float64 effector xyz out
 
 
+FK_BATCH_FACTOR = 8  # FK angle vectors per rank = 8 x the shard's points (8M at the default)
+
+
 def run_fk(job, args):
-    """Batched FK (forward.py:73-94, the DH chain) on as many angle
-    vectors as this rank's shard has points, drawn uniformly in [-pi, pi): its
-    bound is HBM (56 B per point) or the float64 sin/cos + products, whichever is
-    longer.  No collective (each rank its own vectors)."""
+    """Batched FK (forward.py:73-94, the DH chain) on
+    FK_BATCH_FACTOR times as many angle vectors as this rank's shard has points,
+    drawn uniformly in [-pi, pi): its bound is HBM (56 B per point) or the float64
+    sin/cos + products, whichever is longer.  8M vectors make a launch ~0.1 ms, so
+    the dispatch's fixed ~1 us (completion signal) is < 1 % of the kernel time the
+    roofline divides by (at 1M it was 7 %, r06 lease A).  No collective (each rank
+    its own vectors)."""
     import torch
     from inversekinematicsann_amd import _native
-    ctx, world, n = job.ctx, job.world, job.n_local
+    ctx, world, n = job.ctx, job.world, job.n_local * FK_BATCH_FACTOR
     g = torch.Generator(device="cuda")
     g.manual_seed(7)
     dang = (torch.rand((n, 4), generator=g, dtype=torch.float64, device="cuda") * 2 - 1) * math.pi
@@ -668,9 +674,8 @@ def run_fk(job, args):
                        "frac": achieved / HBM_PEAK if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
-                       "kernel_ms_note": "events bracket one launch of 1M points (its fixed "
-                                         "launch cost included); rocprof is the kernel's own "
-                                         "duration",
+                       "kernel_ms_note": "events: the dispatch's own start / end stamps "
+                                         "(hipExtLaunchKernel); rocprof: its kernel trace",
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
                        **prof,
                        "kernel": "fk_kernel", "kernel_ms": k,
@@ -1045,7 +1050,7 @@ def secondary_entry(key, r2, total, world, args):
 DRIVER_TIMEOUT_S = 600  # the driver's limit on one bench.py run (BENCH_r05.json timeout_s)
 # measured per-step times at 1M points per rank (profiles/r05/lease_bench_default.json)
 LEG_STEP_MS = {"ann": 39.2, "fabrik": 0.36, "fabrik_tol1e-5": 0.51, "ann_bf16x6": 21.9,
-               "ann_fp16x3": 12.7, "fk": 0.023}
+               "ann_fp16x3": 12.7, "fk": 0.13}  # (fk: FK_BATCH_FACTOR x the points)
 E2E_BYTES_PER_POINT = {"ann": 24 + 16, "fabrik": 24 + 32}
 PCIE_BYTES_PER_S = 50e9   # tools/pcie_probe.py: ~55 GB/s, the directions do not overlap
 STARTUP_S = 120.0         # first `import torch` + HIP init on a fresh box (1-2 min)

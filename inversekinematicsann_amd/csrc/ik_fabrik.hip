@@ -1218,8 +1218,11 @@ fabrik_iter_kernel(FabArgs a) {
 #endif
     {
       // one divergent region per iteration: lanes that stop here become pending
-      // (parked at the next refill) without a branch of their own
-      const bool run = active && st == IK_OK && cont && (max_iter > step);
+      // (parked at the next refill) without a branch of their own.  (No st test:
+      // every step that sets an error status also clears cont -- the general
+      // step's errors give NaN errors, whose comparisons are false, and the core
+      // step's kStRedo clears it explicitly.)
+      const bool run = active && cont && (max_iter > step);
       pending = pending || (active && !run);
       active = run;
       if (__popcll(__builtin_amdgcn_ballot_w64(!run)) >= need) break;  // (a bool: no VGPR round trip)
@@ -1231,7 +1234,10 @@ fabrik_iter_kernel(FabArgs a) {
           // wave-wide in-loop redo needed one, 7 register moves per iteration)
           uint32_t dom = 0;
           fabrik_step4_lazy(J0, J1, J2, g, L, a.band, bok, tol2, cont, cq, cd, cdom, dom);
-          if (dom >= kCoreDom) st = kStRedo;
+          if (dom >= kCoreDom) {
+            st = kStRedo;
+            cont = false;
+          }
         } else if constexpr (CORE == 1) {
           // wave-uniform fallback: when any lane's radicand leaves sqrt_core's
           // domain (coincident joints, non-finite input) the wave redoes the
