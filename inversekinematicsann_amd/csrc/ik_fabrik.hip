@@ -345,6 +345,7 @@ struct FabArgs {
   double tol2;     // tol_threshold(tol): the loop compares squared errors with it
   ErrBand band;    // the lazy errors' band (fabrik_band) for lanes with |J0|_1 + |goal|_1 <= band_n1
   double band_n1;
+  double qmax;     // the core-domain test on the quotients (fabrik_qmax)
   int max_iter;
   int check_limits;
   double *ang;
@@ -913,6 +914,8 @@ fabrik_iter_kernel(FabArgs a) {
   // canonicalizing) and a compare instead of two compares
   double tol2g = tol2;
   asm volatile("" : "+v"(tol2g));
+  double qmax = a.qmax;  // (CORE 2: fabrik_step4_lazy's domain test, also in a VGPR)
+  asm volatile("" : "+v"(qmax));
   double L[4] = {a.r.links[0], a.r.links[1], a.r.links[2], a.r.links[3]};
 
   // prepared points: the batch's entry j in slot j of the wave's LDS batch
@@ -920,11 +923,13 @@ fabrik_iter_kernel(FabArgs a) {
   struct PrepBatch {  // per entry seven 16-byte words: seed joints 0..2, goal, {meta, cq}
     double2 w[64][7];
   };
-  // an entry's meta word: the point index, and (CORE 2) whether the seed's carried
-  // radicand is outside the core domain (bit 62) and whether the launch's error
-  // band covers the point (bit 61) -- the carry itself (reuse_carry) and the band
-  // test are taken at full width in the preparation, not per refill (r06)
-  constexpr uint64_t kMetaCdomBad = 1ull << 62, kMetaBok = 1ull << 61;
+  // an entry's meta word: the point index, and (CORE 2, bit 62) whether the point
+  // goes straight to the retire step's general re-solve: the seed's carried
+  // radicand outside the core domain, or a start / goal past the launch's error
+  // band (|J0|_1 + |goal|_1 > band_n1, or not finite) -- the carry itself
+  // (reuse_carry) and the band test are taken at full width in the preparation,
+  // not per refill (r06)
+  constexpr uint64_t kMetaRedo = 1ull << 62;
   __shared__ PrepBatch batches[4];
   PrepBatch &PB = batches[threadIdx.x >> 6];
   int pcount = 0, pptr = 0;
@@ -956,17 +961,20 @@ fabrik_iter_kernel(FabArgs a) {
   // step leaves it to the carry: effector() below)
   d3 J0 = {0, 0, 0}, J1 = J0, J2 = J0, J3 = J0, g = J0;
   bool cont = true;  // the reference's loop condition after the lane's last iteration
-  int step = 0, st = IK_OK;
-  double cq = 0.0;  // CORE == 2: the carried quotient, offset and domain value
+  int st = IK_OK;
+  // the lane's iteration count as step - max_iter (mod 2^32): the increment's
+  // carry is the cap (fabrik.py:57 iteration < max_iter), folded into cont, so
+  // the loop's run test needs no compare of its own (r06)
+  uint32_t kst = 0;
+  auto steps = [&]() -> int { return (int)(kst + (uint32_t)max_iter); };
+  double cq = 0.0;  // CORE == 2: the carried quotient and offset
   d3 cd = J0;
-  uint32_t cdom = 0;
-  bool bok = false;  // CORE == 2: the launch's error band covers the lane (fabrik_step4_lazy)
-  // the effector F3 = get_point_between(F2, goal, L3): from the carry (cq, cd =
-  // goal - F2) whenever its radicand was in the core domain, else the fallback's J3
+  bool cbad = false;  // CORE == 2: the taken entry goes to the retire step's re-solve
+  // the effector F3 = get_point_between(F2, goal, L3): CORE 2 from the carry (cq,
+  // cd = goal - F2; a lane whose radicands left the core domain is re-solved at
+  // retire, kStRedo), else the step's J3
   auto effector = [&]() -> d3 {
-    if constexpr (CORE == 2) {
-      if (cdom < kCoreDom) return {J2.x + (cq * cd.x), J2.y + (cq * cd.y), J2.z + (cq * cd.z)};
-    }
+    if constexpr (CORE == 2) return {J2.x + (cq * cd.x), J2.y + (cq * cd.y), J2.z + (cq * cd.z)};
     return J3;
   };
 
@@ -1026,7 +1034,7 @@ fabrik_iter_kernel(FabArgs a) {
           rcnt = 0;
         }
         if (pending)
-          ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, effector(), g, out, step, st);
+          ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, effector(), g, out, steps(), st);
         pending = false;
         rcnt += np;
       }
@@ -1099,13 +1107,12 @@ fabrik_iter_kernel(FabArgs a) {
         g = {w4.y, w5.x, w5.y};
         const double2 w6 = w[6];
         const uint64_t meta = (uint64_t)__double_as_longlong(w6.x);
-        out = (int64_t)(meta & (kMetaBok - 1));
+        out = (int64_t)(meta & (kMetaRedo - 1));
         if constexpr (CORE == 2) {
           // the seed's carry (reuse_carry): cd = goal - J2, exact, as it computes it
           cq = w6.y;
           cd = {g.x - J2.x, g.y - J2.y, g.z - J2.z};
-          cdom = (meta & kMetaCdomBad) ? 0xffffffffu : 0u;
-          bok = (meta & kMetaBok) != 0;
+          cbad = (meta & kMetaRedo) != 0;
         }
       };
       // (read before a preparation overwrites the batch)
@@ -1147,7 +1154,7 @@ fabrik_iter_kernel(FabArgs a) {
             const bool pbok = fabs(Js[0].x) + fabs(Js[0].y) + fabs(Js[0].z) + fabs(ng.x) +
                                   fabs(ng.y) + fabs(ng.z) <=
                               a.band_n1;
-            meta |= (pcdom < kCoreDom ? 0ull : kMetaCdomBad) | (pbok ? kMetaBok : 0ull);
+            meta |= (pcdom < kCoreDom && pbok) ? 0ull : kMetaRedo;
           }
           double2 *w = PB.w[lane];
           w[0] = {Js[0].x, Js[0].y};
@@ -1178,9 +1185,17 @@ fabrik_iter_kernel(FabArgs a) {
       if (mine) {
         st = IK_OK;
         cont = true;  // the loop's initial errors of 1.0 (fabrik.py:53-54) exceed tol
-        step = 0;
+        kst = 0u - (uint32_t)max_iter;
         active = true;
-        // (CORE 2: the carry and the band flag came with the entry, take_entry)
+        // (CORE 2: the carry and the band flag came with the entry, take_entry; a
+        // carry outside the core domain stops the lane before its first iteration,
+        // for the retire step's re-solve)
+        if constexpr (CORE == 2) {
+          if (cbad) {
+            st = kStRedo;
+            cont = false;
+          }
+        }
       }
       IKHIP_MARK("refill.end");
       dry = nstage < 0 && pptr >= pcount;
@@ -1201,12 +1216,14 @@ fabrik_iter_kernel(FabArgs a) {
     // (r06: the loop's control as uint64 wave masks instead of these lane bools
     // measured worse in the ISA: the masks, updated inside the divergent step,
     // went to VGPRs and took ~25 VALU per iteration; the bools live in SGPR lane
-    // masks already, and only ballot(!run) costs a v_cndmask + v_cmp)
+    // masks already, and only ballot(!run) costs a v_cndmask + v_cmp -- also
+    // written as exec & ~ballot(run), and with the band flag as a wave mask taken
+    // at the refill, which put the wave's exec in VGPRs)
     while (true) {
 #ifdef IKHIP_DIAG
     {
       const unsigned long long sm =
-          __ballot(active && st == IK_OK && cont && (max_iter > step));
+          __ballot(active && st == IK_OK && cont);
       IKHIP_DG(kDiagSteps, sm ? 1 : 0);
       IKHIP_DG(kDiagLaneSteps, __popcll(sm));
       if (dry) {  // the queue and the wave's batch are exhausted
@@ -1222,7 +1239,7 @@ fabrik_iter_kernel(FabArgs a) {
       // every step that sets an error status also clears cont -- the general
       // step's errors give NaN errors, whose comparisons are false, and the core
       // step's kStRedo clears it explicitly.)
-      const bool run = active && cont && (max_iter > step);
+      const bool run = active && cont;  // (cont holds the cap: kst)
       pending = pending || (active && !run);
       active = run;
       if (__popcll(__builtin_amdgcn_ballot_w64(!run)) >= need) break;  // (a bool: no VGPR round trip)
@@ -1232,9 +1249,7 @@ fabrik_iter_kernel(FabArgs a) {
           // kStRedo and the retire step re-solves it in the general arithmetic
           // (solve_general), so no copy of the pre-step state is kept (r06: the
           // wave-wide in-loop redo needed one, 7 register moves per iteration)
-          uint32_t dom = 0;
-          fabrik_step4_lazy(J0, J1, J2, g, L, a.band, bok, tol2, cont, cq, cd, cdom, dom);
-          if (dom >= kCoreDom) {
+          if (!fabrik_step4_lazy(J0, J1, J2, g, L, a.band, tol2, qmax, cont, cq, cd)) {
             st = kStRedo;
             cont = false;
           }
@@ -1258,7 +1273,7 @@ fabrik_iter_kernel(FabArgs a) {
           fabrik_step4(J0, J1, J2, J3, g, L, se, ge, st);
           cont = (se > tol2) || (ge > tol2g);
         }
-        ++step;
+        if (__builtin_add_overflow(kst, 1u, &kst)) cont = false;  // max_iter reached
       }
     }
     }
@@ -1276,7 +1291,7 @@ fabrik_iter_kernel(FabArgs a) {
     }
     IKHIP_DT(kDiagTDrain2);
     if (pending)
-      ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, effector(), g, out, step, st);
+      ring_put(R, rcnt + __popcll(pm & lt_mask), J0, J1, J2, effector(), g, out, steps(), st);
     rcnt += np;
     IKHIP_DG(kDiagFlushes, 1);
     IKHIP_DT(kDiagTEnd);
@@ -1371,6 +1386,7 @@ void launch_fabrik_ikine(const RobotDev &r, const double *pts, int64_t n, double
     a.band_n1 = 64.0 * (1.0 + std::fabs(r.dh[4]) + std::fabs(r.dh[8]) + sum_l);
     if (!std::isfinite(a.band_n1)) a.band_n1 = -1.0;  // (no lane: every comparison exact)
     a.band = fabrik_band(a.tol2, a.band_n1, sum_l);
+    a.qmax = fabrik_qmax(r.links);
   }
   a.max_iter = max_iter;
   a.check_limits = check_limits ? 1 : 0;

@@ -100,29 +100,33 @@ namespace ikhip {
 
 // ---- the loop condition without the start and goal errors' own arithmetic ----
 // fabrik.py:57-64 continues while se > tol or ge > tol, se = |B0 - start| and
-// ge = |F3 - goal| (squared here, against tol2).  With q = L0 / |b1 - start| the
-// start error is |(q - 1) (start - b1)| up to roundings, and with the carried
-// quotient cq the goal error is |(cq - 1) (goal - c2)|: sea = |1 - q| sqrt(x) and
-// gea = |1 - cq| sqrt(x3) from the roots the step computes anyway.  The
+// ge = |F3 - goal| (squared here, against tol2).  b0 lies at L0 from b1 towards
+// start, and start at sqrt(x) from b1: se = |sqrt(x) - L0| up to roundings (r06;
+// r05 took |1 - q| sqrt(x), one multiply more and after the division), and the
+// goal error is |sqrt(x3) - L3| with x3 the carried quotient's radicand.  The
 // reference's own se2 / ge2 (b0, F3 = c3 and their differences, 25 VALU) are
 // computed only when an approximation falls inside the launch's band [lo, hi]
 // (ErrBand): outside it the comparison with tol2 provably comes out the same.
 //
 // The band: with u = 2^-53, every rounding of b0 = b1 + q (start - b1), B0 - start,
 // the squares and the root moves |B0 - start| by at most
-//   D <= 1.03 u (3 |goal| + 2 |start| + 3 sum L)
-// (the backward points lie within sum L of the goal, the forward ones within sum L
-// of the start; the same bound with the roles swapped covers the goal error), and
-// sea's own relative error (1 - q, the root, the product) is below 3u.  With
-// T = sqrt(tol2) (real):
+//   1.03 u (3 |goal| + 2 |start| + 3 sum L)
+// from |1 - q| |start - b1| (the backward points lie within sum L of the goal, the
+// forward ones within sum L of the start; the same bound with the roles swapped
+// covers the goal error).  The approximation s - L0 (s = RN(sqrt(x))) is that value
+// up to |s - |start - b1|| <= 2.5 u |start - b1| <= 2.5 u (n1 + sum L) and
+// |q s - L0| <= 3.5 u L0 (x's three roundings, the root's, the quotient's), and
+// rounds itself (relative u).  So with n1 = |start|_1 + |goal|_1 the distance of
+// sea = |s - L0| from the reference's error is at most u (5.6 n1 + 7.4 sum L) + u sea;
+// D is twice the absolute part, D = 2^-52 (6 n1max + 8 sum L + 1), and the relative
+// part (< 2^-52) sits far inside the band's 2^-36.  With T = sqrt(tol2) (real):
 //   sea > hi = (D + T) (1 + 2^-36)        =>  se2 > tol2
 //   sea < lo = (T - D) (1 - 2^-36)        =>  se2 <= tol2   (only if D <= T / 2)
-// (tests/test_band_cpu.py checks the bound along real iterations: the gap stays
-// below 0.17 D.)  The band is one per launch (fabrik_band on the host): D from a
-// bound n1max on |start|_1 + |goal|_1, D = 2u (3 n1max + 4 sum L + 1) (twice the
-// bound; L1 norms bound the Euclidean ones), with T's bounds tol_lo <= T <= tol_hi.
-// A lane past n1max (or with a non-finite goal) carries bok = false: its
-// comparisons are exact.
+// (tests/test_band_cpu.py checks the bound along real iterations.)  The band is one
+// per launch (fabrik_band on the host): n1max bounds |start|_1 + |goal|_1 (L1 norms
+// bound the Euclidean ones), with T's bounds tol_lo <= T <= tol_hi.  A lane past
+// n1max (or with a non-finite goal) never runs this step: the iteration kernel hands
+// it to the retire step's general re-solve (r06; r05 made its comparisons exact).
 struct ErrBand {
   double lo, hi;
 };
@@ -130,68 +134,85 @@ struct ErrBand {
 __host__ __forceinline__ ErrBand fabrik_band(double tol2, double n1max, double sum_l) {
   // tol2 <= 0 (tol = 0, or a negative tol): a band that decides nothing, every
   // comparison exact.  (hi = 0 would call any sea > 0 "above", but at tol = 0 the
-  // reference stops where b0 rounds onto start exactly, se2 == 0, while q is
-  // 1 +- 1 ulp and sea > 0: ADVICE r05.)
+  // reference stops where b0 rounds onto start exactly, se2 == 0, while s is
+  // L0 +- 1 ulp and sea > 0: ADVICE r05.)
   ErrBand b = {-1.0, INFINITY};
   if (!(tol2 > 0.0)) return b;
   const double T = std::sqrt(tol2);
   const double tol_lo = T * (1.0 - 0x1p-50), tol_hi = T * (1.0 + 0x1p-50);
-  const double d = 0x1p-52 * (3.0 * n1max + 4.0 * sum_l + 1.0);
+  const double d = 0x1p-52 * (6.0 * n1max + 8.0 * sum_l + 1.0);
   b.hi = (d + tol_hi) * (1.0 + 0x1p-36);
   b.lo = (d <= 0.5 * tol_lo) ? (tol_lo - d) * (1.0 - 0x1p-36) : -1.0;
   return b;
 }
 
+// The core domain from the quotients (r06): a radicand x outside sqrt_core's
+// domain (0, tiny, inf, NaN) gives a quotient L / sqrt_core(x) that is NaN or
+// larger in magnitude than |L| 2^382 (tools/dom_check.hip, every binade below
+// 2^-767 and the specials on gfx950), and an in-domain one a quotient at most
+// |L| 2^383.5.  So |q1| + |q| + |q2| + |cq| <= qmax = min |L| 2^382 (fabrik_qmax)
+// implies every radicand of the iteration is >= 2^-764 and finite: in the
+// domain.  Lanes that fail it (the true out-of-domain ones and any in
+// [2^-767, 2^-764)) are re-solved in the general arithmetic (kStRedo): the same
+// bits either way.  3 adds and a compare instead of four exponent extractions,
+// their maximum and a compare.
+__host__ __forceinline__ double fabrik_qmax(const double *L) {
+  double m = std::fabs(L[0]);
+  for (int k = 1; k < 4; ++k) m = std::fmin(m, std::fabs(L[k]));
+  return m * 0x1p382;
+}
+
 // fabrik_step4_reuse with the loop condition cont = (se2 > tol2) || (ge2 > tol2)
-// decided through the band, and F3 (c3 = c2 + cq cd, the reference's
-// get_point_between(c2, goal, L3) from the carry) left to the caller.  The exact
-// se2 / ge2 run in a wave-uniform branch when any lane's approximation is uncertain
-// (and for the goal error only where the start error has not already decided).
-__device__ __forceinline__ void fabrik_step4_lazy(const d3 start, d3 &c1, d3 &c2, const d3 g,
+// decided through the band, the core domain from the quotients, and F3 (c3 = c2 +
+// cq cd, the reference's get_point_between(c2, goal, L3) from the carry) left to
+// the caller.  The exact se2 / ge2 run in a wave-uniform branch when any lane's
+// approximation is uncertain (and for the goal error only where the start error
+// has not already decided).  Returns whether the iteration's radicands were all
+// in the core domain.  (The masks are formed right before their branches: held
+// longer, or with the wave's exec taken once, they went to VGPRs, r06.)
+__device__ __forceinline__ bool fabrik_step4_lazy(const d3 start, d3 &c1, d3 &c2, const d3 g,
                                                   const double *L, const ErrBand band,
-                                                  bool bok, double tol2, bool &cont, double &cq, d3 &cd,
-                                                  uint32_t &cdom, uint32_t &dom) {
-  dom = cdom;
+                                                  double tol2, double qmax,
+                                                  bool &cont, double &cq, d3 &cd) {
   const d3 b2 = {g.x - cq * cd.x, g.y - cq * cd.y, g.z - cq * cd.z};
-  const d3 b1 = point_between_core(b2, c1, L[1], dom);
+  const double ux = c1.x - b2.x, uy = c1.y - b2.y, uz = c1.z - b2.z;
+  const double q1 = div_core(L[1], sqrt_core(sq(ux) + sq(uy) + sq(uz)));
+  const d3 b1 = {b2.x + (q1 * ux), b2.y + (q1 * uy), b2.z + (q1 * uz)};
   const double dx = start.x - b1.x, dy = start.y - b1.y, dz = start.z - b1.z;
-  const double x = sq(dx) + sq(dy) + sq(dz);
-  dom = max(dom, sqrt_core_dom(x));
-  const double sx = sqrt_core(x);
+  const double sx = sqrt_core(sq(dx) + sq(dy) + sq(dz));
   const double q = div_core(L[0], sx);
   const double qx = q * dx, qy = q * dy, qz = q * dz;
   // the decisions as lane masks (ballots of the compares): the band tests, the
   // merges with the exact results and the uncertainty are scalar-ALU operations
   const uint64_t ex = __builtin_amdgcn_read_exec();
-  const uint64_t nbok = __builtin_amdgcn_ballot_w64(!bok);
-  const double sea = fabs(1.0 - q) * sx;  // |B0 - start| from the radicand's root
+  const double sea = fabs(sx - L[0]);  // |B0 - start| up to the band
   uint64_t gt = __builtin_amdgcn_ballot_w64(sea > band.hi);
-  uint64_t unc = (ex & ~(gt | __builtin_amdgcn_ballot_w64(sea < band.lo))) | nbok;
+  uint64_t unc = ex & ~(gt | __builtin_amdgcn_ballot_w64(sea < band.lo));
   if (__builtin_expect(unc != 0, 0)) {  // (a NaN is uncertain)
     const d3 b0 = {b1.x + qx, b1.y + qy, b1.z + qz};
     const double se2 = dist3_sq(b0, start);
     gt = (gt & ~unc) | (__builtin_amdgcn_ballot_w64(se2 > tol2) & unc);
   }
   c1 = {start.x - qx, start.y - qy, start.z - qz};
-  c2 = point_between_core(c1, b2, L[2], dom);
+  const double vx = b2.x - c1.x, vy = b2.y - c1.y, vz = b2.z - c1.z;
+  const double q2 = div_core(L[2], sqrt_core(sq(vx) + sq(vy) + sq(vz)));
+  c2 = {c1.x + (q2 * vx), c1.y + (q2 * vy), c1.z + (q2 * vz)};
   const double ex3 = g.x - c2.x, ey3 = g.y - c2.y, ez3 = g.z - c2.z;
-  const double x3 = sq(ex3) + sq(ey3) + sq(ez3);
-  cdom = sqrt_core_dom(x3);
-  dom = max(dom, cdom);
-  const double sx3 = sqrt_core(x3);
+  const double sx3 = sqrt_core(sq(ex3) + sq(ey3) + sq(ez3));
   cq = div_core(L[3], sx3);
   cd = {ex3, ey3, ez3};
-  const double gea = fabs(1.0 - cq) * sx3;  // |F3 - goal|
+  const double gea = fabs(sx3 - L[3]);  // |F3 - goal| up to the band
   uint64_t gt3 = __builtin_amdgcn_ballot_w64(gea > band.hi);
   // (the goal error only matters where the start error has not decided already)
   uint64_t unc3 =
-      ((ex & ~(gt3 | __builtin_amdgcn_ballot_w64(gea < band.lo))) | nbok) & ~gt;
+      ex & ~(gt3 | __builtin_amdgcn_ballot_w64(gea < band.lo) | gt);
   if (__builtin_expect(unc3 != 0, 0)) {
     const d3 c3 = {c2.x + (cq * ex3), c2.y + (cq * ey3), c2.z + (cq * ez3)};
     const double ge2 = dist3_sq(c3, g);
     gt3 = (gt3 & ~unc3) | (__builtin_amdgcn_ballot_w64(ge2 > tol2) & unc3);
   }
   cont = __builtin_amdgcn_inverse_ballot_w64(gt | gt3);
+  return (fabs(q1) + fabs(q)) + (fabs(q2) + fabs(cq)) <= qmax;
 }
 
 }  // namespace ikhip

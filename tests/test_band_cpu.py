@@ -1,8 +1,9 @@
 """The FABRIK loop condition's error band (csrc/ik_fabrik_step.h, fabrik_step4_lazy /
 fabrik_band), checked numerically on the CPU: along real FABRIK iterations (numpy
 float64, the reference's arithmetic: kinematics/point.py:25-45, fabrik.py:19-64),
-the start and goal errors the step approximates from its radicands,
-|1 - q| sqrt(x) and |1 - cq| sqrt(x3), stay within the band's D of the reference's own
+the start and goal errors the step approximates from its radicands' roots,
+|sqrt(x) - L0| and |sqrt(x3) - L3| (r06; r05: |1 - q| sqrt(x)), stay within the band's
+D of the reference's own
 |B0 - start| and |F3 - goal|, and the band's decisions agree with the exact
 comparison for thresholds placed right at the errors.  The GPU tests check the
 kernel bit for bit; this pins the bound the kernel's proof rests on, including the
@@ -27,7 +28,7 @@ def band(tol2, n1max, sum_l):
         return -1.0, np.inf, 0.0  # decides nothing: every comparison exact
     T = np.sqrt(tol2)
     tlo, thi = T * (1.0 - 2.0 ** -50), T * (1.0 + 2.0 ** -50)
-    d = 2.0 ** -52 * (3.0 * n1max + 4.0 * sum_l + 1.0)
+    d = 2.0 ** -52 * (6.0 * n1max + 8.0 * sum_l + 1.0)
     hi = (d + thi) * (1.0 + 2.0 ** -36)
     lo = (tlo - d) * (1.0 - 2.0 ** -36) if d <= 0.5 * tlo else -1.0
     return lo, hi, d
@@ -57,13 +58,13 @@ def test_band_bounds_the_approximate_errors():
         b1, _, _ = pb(b2, c1, L)
         b0, x, q = pb(b1, start, L)
         se = np.sqrt(((b0 - start) ** 2).sum(1))
-        sea = np.abs(1.0 - q) * np.sqrt(x)
+        sea = np.abs(np.sqrt(x) - L)
         c1, _, _ = pb(start, b1, L)
         c2, _, _ = pb(c1, b2, L)
         c3, x3, cq = pb(c2, g, L)
         ge = np.sqrt(((c3 - g) ** 2).sum(1))
-        gea = np.abs(1.0 - cq) * np.sqrt(x3)
-        d = 2.0 ** -52 * (3.0 * n1 + 4.0 * 4 * L + 1.0)
+        gea = np.abs(np.sqrt(x3) - L)
+        d = 2.0 ** -52 * (6.0 * n1 + 8.0 * 4 * L + 1.0)
         ok = np.isfinite(se) & np.isfinite(ge)
         # the kernel's D is twice the bound it needs; the observed gap stays below half
         r = np.maximum(np.abs(se - sea), np.abs(ge - gea))[ok] / d[ok]
@@ -76,7 +77,7 @@ def test_band_decisions_match_exact_comparisons():
     """Thresholds from 1e-6 relative down to one ulp around the errors themselves:
     wherever the band decides, it decides as the exact squared comparison does (and
     the thresholds closest to the error are left to the exact comparison).  The
-    approximation is the kernel's root-space one, |1 - q| sqrt(x), against the
+    approximation is the kernel's root-space one, |sqrt(x) - L0|, against the
     un-squared band; the exact comparison is the squared one."""
     rng = np.random.default_rng(6)
     L = 2.0
@@ -91,7 +92,7 @@ def test_band_decisions_match_exact_comparisons():
         b1, _, _ = pb(b2, c1, L)
         b0, x, q = pb(b1, start, L)
         se2 = ((b0 - start) ** 2).sum(1)
-        sea = np.abs(1.0 - q) * np.sqrt(x)
+        sea = np.abs(np.sqrt(x) - L)
         c1, _, _ = pb(start, b1, L)
         c2, _, _ = pb(c1, b2, L)
         for k in range(0, len(se2), 97):
@@ -140,7 +141,7 @@ def test_band_at_tol_zero_decides_nothing():
         b1, _, _ = pb(b2, c1, L)
         b0, x, q = pb(b1, start, L)
         se2 = ((b0 - start) ** 2).sum(1)
-        sea = np.abs(1.0 - q) * np.sqrt(x)
+        sea = np.abs(np.sqrt(x) - L)
         zero += int((se2 == 0.0).sum())
         # at tol2 = 0 the band never claims a decision
         assert not (sea > hi).any() and not (sea < lo).any()

@@ -1,4 +1,4 @@
-# r06 A/B lease: the GPU tests on the working tree's build, then FABRIK (rocprof
+# r06 A/B lease (ANN=0 skips the ANN runs, TESTS=0 the tests, BENCH=0 the bench): the GPU tests on the working tree's build, then FABRIK (rocprof
 # kernel averages, tools/fab_ab_prof.sh) and ANN split modes (tools/ann_ab.sh)
 # for libikhip_prev.so (tools/build_prev.sh: git HEAD) against libikhip.so,
 # interleaved twice, then the default bench line.  Stops at the first crash.
@@ -13,6 +13,7 @@ if [ "${TESTS:-1}" = 1 ]; then
 fi
 for rep in 1 2; do
   if [ "${FAB:-1}" = 1 ]; then bash tools/fab_ab_prof.sh gpurun_out/fabprof_$rep ${LIBS:-libikhip_prev.so libikhip.so} || exit $?; fi
+  [ "${ANN:-1}" = 1 ] || continue
   for m in ${ANN_MODES:-bf16x6}; do
     MODE=$m STEPS=10 bash tools/ann_ab.sh ${ANN_SPECS:-${LIBS:-libikhip_prev.so libikhip.so}} || exit $?
   done

@@ -1,0 +1,105 @@
+// dom_check.hip -- the FABRIK iteration's core-domain test from the quotients:
+// for every radicand x below sqrt_core's domain (0 < x < 2^-767, subnormals
+// included), is q = div_core(L, sqrt_core(x)) NaN or larger in magnitude than
+// |L| 2^382?  (ik_fabrik_step.h, fabrik_step4_lazy: the lane leaves the core
+// path when |q1| + |q| + |q2| + |cq| is not <= min|L| 2^382, which is then
+// equivalent to "some radicand is outside [2^-764, 2^1024)" up to lanes flagged
+// needlessly -- those are re-solved in the general arithmetic with the same bits.)
+// Also x = 0, inf and NaN.  Prints one JSON line per link length; exit 1 on a miss.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/dom_check tools/dom_check.hip
+//   tools/dom_check [log2 radicands per link length, default 30]
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "../inversekinematicsann_amd/csrc/ik_common.h"
+
+using namespace ikhip;
+
+__device__ __forceinline__ uint64_t mix(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void check(double L, uint64_t per_thread, uint64_t seed,
+                                             unsigned long long *cnt, double *first) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const double qmax = fabs(L) * 0x1p382;
+  unsigned long long miss = 0, flagged_in = 0, nan = 0;
+  for (uint64_t k = 0; k < per_thread; ++k) {
+    const uint64_t r = mix(seed ^ (tid * 0x100000001b3ull + k));
+    // biased exponents 0 (subnormal) .. 259: the 256 below the domain's 2^-767 and
+    // four binades inside it
+    const uint64_t e = (r >> 52) % 260;
+    uint64_t mant = r & 0xfffffffffffffull;
+    if (e == 0 && mant == 0) mant = 1;
+    const double x = __longlong_as_double((long long)((e << 52) | mant));
+    const double q = div_core(L, sqrt_core(x));
+    const bool pass = fabs(q) <= qmax;  // the kernel's test (NaN fails it)
+    nan += isnan(q) ? 1ull : 0ull;
+    if (e < 256) {  // below the domain: must fail the test
+      if (pass) {
+        ++miss;
+        if (atomicAdd(&cnt[3], 1ull) == 0) {
+          first[0] = x;
+          first[1] = q;
+        }
+      }
+    } else if (!pass) {
+      ++flagged_in;
+    }
+  }
+  atomicAdd(&cnt[0], miss);
+  atomicAdd(&cnt[1], flagged_in);
+  atomicAdd(&cnt[2], nan);
+}
+
+__global__ void specials(double L, double *out) {
+  const double xs[3] = {0.0, INFINITY, NAN};
+  for (int i = 0; i < 3; ++i) out[i] = div_core(L, sqrt_core(xs[i]));
+}
+
+int main(int argc, char **argv) {
+  const int lg = argc > 1 ? atoi(argv[1]) : 30;
+  const unsigned blocks = 4096, threads = 256;
+  const uint64_t per_thread = ((1ull << lg) + blocks * threads - 1) / (blocks * threads);
+  const double Ls[] = {1.0, 2.0, 0.7, -3.25, 0x1p-100, 0x1p100, 1.0 / 3.0};
+  unsigned long long *cnt;
+  double *first, *sp;
+  hipMalloc(&cnt, 4 * sizeof(unsigned long long));
+  hipMalloc(&first, 2 * sizeof(double));
+  hipMalloc(&sp, 3 * sizeof(double));
+  int rc = 0;
+  for (double L : Ls) {
+    hipMemset(cnt, 0, 4 * sizeof(unsigned long long));
+    hipLaunchKernelGGL(check, dim3(blocks), dim3(threads), 0, 0, L, per_thread,
+                       0xd0d0ull ^ (uint64_t)(L * 1e6), cnt, first);
+    hipLaunchKernelGGL(specials, dim3(1), dim3(1), 0, 0, L, sp);
+    if (hipDeviceSynchronize() != hipSuccess) {
+      fprintf(stderr, "kernel failed\n");
+      return 2;
+    }
+    unsigned long long h[4];
+    double f[2], s[3];
+    hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost);
+    hipMemcpy(f, first, sizeof f, hipMemcpyDeviceToHost);
+    hipMemcpy(s, sp, sizeof s, hipMemcpyDeviceToHost);
+    const bool sp_ok = !(std::fabs(s[0]) <= std::fabs(L) * 0x1p382) &&
+                       !(std::fabs(s[1]) <= std::fabs(L) * 0x1p382) &&
+                       !(std::fabs(s[2]) <= std::fabs(L) * 0x1p382);
+    printf("{\"L\": %.17g, \"radicands\": %llu, \"below_domain_passed\": %llu, "
+           "\"in_domain_flagged\": %llu, \"nan\": %llu, \"q(0,inf,nan)\": [%g, %g, %g], "
+           "\"specials_flagged\": %s",
+           L, (unsigned long long)(per_thread * blocks * threads), h[0], h[1], h[2], s[0], s[1],
+           s[2], sp_ok ? "true" : "false");
+    if (h[0]) printf(", \"first\": [%.17g, %.17g]", f[0], f[1]);
+    printf("}\n");
+    if (h[0] || !sp_ok) rc = 1;
+  }
+  return rc;
+}
