@@ -148,3 +148,28 @@ def test_band_at_tol_zero_decides_nothing():
         c1, _, _ = pb(start, b1, L)
         c2, _, _ = pb(c1, b2, L)
     assert zero > 0  # converged chains do reach se2 == 0, where tol 0 can stop
+
+
+def test_quotient_domain_test_evidence():
+    """The iteration's core-domain test reads the quotients (ik_fabrik_step.h,
+    fabrik_step4_lazy / fabrik_qmax, r06): |q1| + |q| + |q2| + |cq| <= min|L| 2^382.
+    It is sound only if every radicand below sqrt_core's domain gives a quotient
+    that is NaN or above |L| 2^382 on the hardware -- a property of v_rsq_f64 /
+    v_rcp_f64 that no CPU can restate.  tools/dom_check.hip measured it on gfx950
+    (2^30 radicands per link length over every binade below 2^-767, subnormals
+    included, and 0 / inf / NaN); this pins the committed record and the source's
+    threshold."""
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rows = [json.loads(l) for l in open(os.path.join(root, "profiles", "r06", "ab",
+                                                     "dom_check.json"))]
+    assert len(rows) >= 5
+    for r in rows:
+        assert r["below_domain_passed"] == 0, r
+        assert r["specials_flagged"] is True, r
+        assert r["radicands"] >= 2 ** 30
+    assert any(abs(r["L"]) < 2.0 ** -90 for r in rows) and any(abs(r["L"]) > 2.0 ** 90 for r in rows)
+    src = open(os.path.join(root, "inversekinematicsann_amd", "csrc", "ik_fabrik_step.h")).read()
+    assert "return m * 0x1p382;" in src
+    assert "(fabs(q1) + fabs(q)) + (fabs(q2) + fabs(cq)) <= qmax" in src
