@@ -162,8 +162,11 @@ def test_quotient_domain_test_evidence():
     import json
     import os
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    rows = [json.loads(l) for l in open(os.path.join(root, "profiles", "r06", "ab",
-                                                     "dom_check.json"))]
+    import re
+    # (the specials' quotients print as C's nan / -nan, not JSON: dropped, their verdict
+    # is specials_flagged)
+    rows = [json.loads(re.sub(r'"q\(0,inf,nan\)": \[[^\]]*\], ', "", l))
+            for l in open(os.path.join(root, "profiles", "r06", "ab", "dom_check.json"))]
     assert len(rows) >= 5
     for r in rows:
         assert r["below_domain_passed"] == 0, r

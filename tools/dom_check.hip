@@ -93,7 +93,7 @@ int main(int argc, char **argv) {
                        !(std::fabs(s[1]) <= std::fabs(L) * 0x1p382) &&
                        !(std::fabs(s[2]) <= std::fabs(L) * 0x1p382);
     printf("{\"L\": %.17g, \"radicands\": %llu, \"below_domain_passed\": %llu, "
-           "\"in_domain_flagged\": %llu, \"nan\": %llu, \"q(0,inf,nan)\": [%g, %g, %g], "
+           "\"in_domain_flagged\": %llu, \"nan\": %llu, \"q(0,inf,nan)\": [\"%g\", \"%g\", \"%g\"], "
            "\"specials_flagged\": %s",
            L, (unsigned long long)(per_thread * blocks * threads), h[0], h[1], h[2], s[0], s[1],
            s[2], sp_ok ? "true" : "false");
