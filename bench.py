@@ -1194,6 +1194,10 @@ def main():
                    "points_per_gpu": hi - lo, "total_points": total,
                    "parallelism": f"dp{world}", "method": args.method,
                    "ann_mode": args.ann_mode if args.method == "ann" else None,
+                   # a gloo rehearsal with more ranks than GPUs: the ranks share a
+                   # device, so per-rank kernel durations (and fracs) are not one GPU's
+                   **({"devices_shared": world // max(1, torch.cuda.device_count())}
+                      if world > torch.cuda.device_count() else {}),
                    "all_gather_in_step": sc is not None,
                    "collective": ("RCCL all-gathers inside libikhip (ik_*_solve_sharded): each "
                                   "chunk's angles (+ FABRIK iterations) gathered in place under "

@@ -252,7 +252,10 @@ def test_committed_bench_lines_kernel_fits_step():
             fe, fr = rf.get("frac_events"), rf.get("frac_rocprof")
             # (against a rocprof profile of this round's kernels only)
             same_round = str(rf.get("profile", "")).startswith("profiles/r06")
-            if fe and fr and same_round and name in ("headline", "fabrik", "fabrik_tol1e-5", "fk"):
+            # (a rehearsal whose ranks share one device times each kernel under the
+            # other ranks' load: config.devices_shared; its durations still fit)
+            shared = bool(d.get("config", {}).get("devices_shared"))
+            if fe and fr and same_round and not shared and name in ("headline", "fabrik", "fabrik_tol1e-5", "fk"):
                 assert abs(fe / fr - 1.0) <= 0.05, (path, name, fe, fr)
 
 

@@ -14,5 +14,6 @@ timeout -k 10 300 python bench.py > gpurun_out/bench_confirm.json 2> gpurun_out/
 rc=$?; echo "bench rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi
 # the N > 1 launcher and bookkeeping on one GPU: two gloo ranks share device 0 (RCCL
 # takes one rank per GPU, so --gather 0)
-IKHIP_DIST_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 --gather 0 --secondary 0 --cpu-seconds 0 --end-to-end 0 --steps 3 --warmup 1 > gpurun_out/bench_2rank_gloo.json 2> gpurun_out/bench_2rank_gloo.err
+# (every leg of the N > 1 line: secondaries, strong legs, end-to-end, cold calls)
+IKHIP_DIST_BACKEND=gloo timeout -k 10 500 python bench.py --gpus 2 --gather 0 --steps 5 --warmup 2 > gpurun_out/bench_2rank_gloo.json 2> gpurun_out/bench_2rank_gloo.err
 rc=$?; echo "2-rank rehearsal rc=$rc"; exit $rc
