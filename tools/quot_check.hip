@@ -1,4 +1,4 @@
-// quot_check.hip -- is quot_sqrt_core(a, x) (ik_common.h: the quotient
+// quot_check.hip -- is quot_sqrt_core(a, x) (tools/quot_fused.h: the quotient
 // a / sqrt(x) with the divisor's reciprocal seeded from sqrt_core's own
 // refined 1/(2 sqrt(x)) instead of v_rcp_f64) bit-identical to
 // div_core(a, sqrt_core(x)) and to the compiler's a / sqrt(x)?  Counts
@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "../inversekinematicsann_amd/csrc/ik_common.h"
+#include "quot_fused.h"
 
 using namespace ikhip;
 

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "../inversekinematicsann_amd/csrc/ik_common.h"
+#include "quot_fused.h"
 
 using namespace ikhip;
 
