@@ -1,6 +1,7 @@
 """bench.py's cpu_baseline leg on the CPU (no GPU): the oracle timed on a bounded
 sample, its thread count, and the parity fields it computes against a GPU batch
 (here the oracle's own output stands in for the GPU's)."""
+import json
 import os
 import sys
 
@@ -275,3 +276,27 @@ def test_wall_budget_fits_the_driver_limit():
     # the library's default deadline (ik_shard.hip) is the one the budget assumes
     src = open(os.path.join(ROOT, "inversekinematicsann_amd", "csrc", "ik_shard.hip")).read()
     assert "env = v > 0.0 ? v : 120.0;" in src
+
+
+def test_rocprof_median_over_boxes():
+    """The committed r06 traffic.json carries each kernel's rocprof window average on
+    several boxes (tools/merge_boxes.py: the profiling lease's first, then the
+    tools/trace_box.sh boxes) and their median; bench.profile_fields prices
+    frac_rocprof on the median and reports the list (a driver box is one more draw)."""
+    import statistics
+    import bench
+    path = os.path.join(ROOT, "profiles", "r06", "traffic.json")
+    t = json.load(open(path))
+    for k in ("ann_fused_kernel", "fabrik_iter_kernel", "fabrik_tol1e-5/fabrik_iter_kernel",
+              "fk_kernel"):
+        v = t[k]
+        assert len(v["rocprof_boxes_ms"]) >= 4 and v["rocprof_boxes_ms"][0] == v["rocprof_avg_ms"]
+        assert v["rocprof_median_ms"] == statistics.median(v["rocprof_boxes_ms"])
+        pf = bench.profile_fields(path, k)
+        assert pf["rocprof_avg_ms"] == v["rocprof_median_ms"]
+        assert pf["rocprof_boxes_ms"] == v["rocprof_boxes_ms"]
+    # a profile without the boxes keeps its own window average
+    lb = os.path.join(ROOT, "profiles", "r06", "lease_b", "traffic.json")
+    pf = bench.profile_fields(lb, "fabrik_iter_kernel")
+    assert pf["rocprof_avg_ms"] == json.load(open(lb))["fabrik_iter_kernel"]["rocprof_avg_ms"]
+    assert "rocprof_boxes_ms" not in pf
