@@ -5,6 +5,7 @@
 //               independent chains per lane, with the production kernel's
 //               per-iteration wave-uniform domain vote: is the iteration
 //               latency-bound (more waves / chains help) or issue-bound?
+//  iterl W      the r06 step (fabrik_step4_lazy) at W waves per SIMD: the loop's own rate
 //  act   V W    the tanh epilogue of the ANN split modes, 8 elements per lane in
 //               flight like act_apply2x4: V 0 = sign (1-e)/(1+e) (r02), 1 = 1 - 2/(1+e),
 //               2 = 1 - 2/(1+e) with e = exp2 from a degree-6 polynomial on the
@@ -77,6 +78,35 @@ __global__ __launch_bounds__(256) void iter_bench(int iters, const double *goals
 #pragma unroll
   for (int k = 0; k < ILP; ++k) s += J3[k].x + J3[k].y + J3[k].z;
   out[tid] = s;
+  if (tid == 0) clk[0] = t1 - t0;
+}
+
+// iterl: the r06 production step (fabrik_step4_lazy: errors from the roots, the
+// quotient domain test, the band decisions as ballots) with the kernel's stop rule
+// (a lane that stops keeps its state; the wave goes on while any lane runs), every
+// lane iterating the same goal set: the loop's own issue rate, against which the
+// iteration kernel's wave-iterations per SIMD cycle are compared.
+__global__ __launch_bounds__(256) void iter_lazy_bench(int iters, const double *goals, int ng,
+                                                       double *out, unsigned long long *clk,
+                                                       ErrBand band, double tol2, double qmax) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const d3 start = {0.0, 0.0, 2.0};
+  const double L[4] = {2.0, 2.0, 2.0, 2.0};
+  const int i = tid % ng;
+  const d3 g = {goals[3 * i], goals[3 * i + 1], goals[3 * i + 2]};
+  d3 J1 = {1e-16, 0.0, 4.0}, J2 = {2e-16, 0.0, 6.0}, cd;
+  double cq;
+  uint32_t cdom;
+  reuse_carry(J2, g, L[3], cq, cd, cdom);
+  double acc = 0.0;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < iters; ++it) {
+    bool cont = true;
+    if (!fabrik_step4_lazy(start, J1, J2, g, L, band, tol2, qmax, cont, cq, cd)) acc += 1.0;
+    acc += cont ? 1.0 : 0.0;
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  out[tid] = acc + J2.x + J2.y + J2.z + cq;
   if (tid == 0) clk[0] = t1 - t0;
 }
 
@@ -453,6 +483,24 @@ int main(int argc, char **argv) {
         };
         timed("iter", L, dclk, lane_it, simd_wave_it, extra);
       }
+  }
+  if (!strcmp(what, "all") || !strcmp(what, "iterl")) {
+    const int iters = 400;
+    const double tol2 = 1e-6;  // tol 1e-3 (the threshold's exact value does not matter here)
+    const ErrBand band = fabrik_band(tol2, 64.0 * 11.0, 8.0);
+    const double Ls[4] = {2.0, 2.0, 2.0, 2.0};
+    const double qmax = fabrik_qmax(Ls);
+    for (int W = 1; W <= 3; ++W) {
+      const unsigned blocks = (unsigned)cus * W;
+      snprintf(extra, sizeof extra, "\"waves_per_simd\": %d", W);
+      const double lane_it = (double)blocks * 256 * iters;
+      const double simd_wave_it = (double)W * iters;
+      auto L = [&]() {
+        hipLaunchKernelGGL(iter_lazy_bench, dim3(blocks), dim3(256), 0, 0, iters, dgoals, ng,
+                           dout, dclk, band, tol2, qmax);
+      };
+      timed("iterl", L, dclk, lane_it, simd_wave_it, extra);
+    }
   }
   if (!strcmp(what, "all") || !strcmp(what, "act")) {
     const int iters = 2000;
