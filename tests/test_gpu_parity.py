@@ -68,6 +68,27 @@ def test_fabrik_vs_oracle_random(ctx):
         assert np.abs(jo - rjo).max() <= 1e-9
 
 
+def test_fabrik_vs_oracle_tight_tolerances(ctx):
+    """Deeper convergence than the BASELINE configs (tol 1e-7 / 300 and 1e-9 / 400):
+    more iterations per goal, errors near the band's width (D ~ 1e-12), and the
+    closed-form seed's last-bit difference from the reference's chain given the most
+    iterations to show: iteration counts still bit-exact with the C oracle, angles
+    and joints within 1e-9, on random_dist and uniform-box goals."""
+    from inversekinematicsann_amd.robot.position_generator import random_dist
+    rng = np.random.default_rng(17)
+    pts = np.concatenate([random_dist(12_000, seed=17),
+                          rng.uniform([0.0, -6.0, -3.0], [6.0, 6.0, 6.0], size=(4_000, 3))])
+    for tol, mi in ((1e-7, 300), (1e-9, 400)):
+        ang, it, jo, st = ctx.fabrik_solve(pts, tol, mi, want_joints=True)
+        rang, rit, rjo, rst = O.fabrik_ikine(pts, tol, mi)
+        assert np.array_equal(it, rit), (tol, int((it != rit).sum()))
+        for a_, r_ in ((ang, rang), (jo, rjo)):  # (NaN where the reference raises)
+            a_, r_ = np.asarray(a_).reshape(len(pts), -1), np.asarray(r_).reshape(len(pts), -1)
+            assert np.array_equal(np.isnan(a_), np.isnan(r_))
+            ok = ~np.isnan(r_)
+            assert np.abs(a_[ok] - r_[ok]).max() <= 1e-9
+
+
 def test_fabrik_tol_zero_and_negative():
     """tol = 0 (and tols whose threshold rounds to 0, or below it) is accepted by
     the reference (fabrik.py:57: the loop then stops only where both errors are
@@ -76,8 +97,9 @@ def test_fabrik_tol_zero_and_negative():
     CORE 2) gives the same iteration counts and the same bits as the kernel that
     compares every error exactly (simple), on every point.  Against the oracle the
     counts cannot be bit-exact at tol 0 alone: whether a chain lands on an exact
-    fixed point depends on every bit of its trajectory, and the seed's cos / sin /
-    atan2 (ocml) may differ from glibc's in the last ulp; so there
+    fixed point depends on every bit of its trajectory, and the closed-form seed
+    (Rz(theta_1) P_k) differs from the reference's chain in the last
+    bits of x / y; so there
     the angles are checked (<= 1e-9) and the points whose counts differ must be
     few and must have converged in one of the two runs."""
     from inversekinematicsann_amd import _native
