@@ -880,10 +880,11 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 
 // ORD: the queue is a.perm (work order above), else point order.  CORE: 0
 // general sqrt / division, 1 sqrt_core / div_core, 2 the same with the repeated
-// distances taken once (fabrik_step4_reuse; needs L0 == L1 and L2 == L3).
+// distances taken once and the loop condition from the band (fabrik_step4_lazy;
+// needs L0 == L1 and L2 == L3).
 // Every solve reaching this kernel runs at least one iteration (the host sends
 // the others to fabrik_simple_kernel), so the seed's last joint is never needed.
-#ifndef IKHIP_FAB_REFILL  // free lanes that trigger a refill (r05: 12 against 6 / 8 / 16 / 20 / 24 / 32; 12 since the dry waves' raised priority)
+#ifndef IKHIP_FAB_REFILL  // free lanes that trigger a refill (r05: 12 against 6 / 8 / 16 / 20 / 24 / 32; 12 since the dry waves' raised priority; r06 on the 142-VALU loop: 8 +1.5-4 %, 16 even-+1.4 %)
 #define IKHIP_FAB_REFILL 12
 #endif
 #ifndef IKHIP_ITER_WAVES
@@ -893,8 +894,9 @@ __device__ __forceinline__ void ring_flush(const FabArgs &a, RetireRing &R, int 
 // angles steps: its dependent chains issue when ready instead of in the partner's
 // leftover slots.  r04, same box: iteration kernel -1.7 % at tol 1e-3, -1.3 % at 1e-5
 // (rocprof windows, 3 / 2 runs each), -1.0 / -1.3 % per bench step in another lease.
-// (Taking the seed's carried quotient in the prepare step instead of at the
-// hand-out measured slower: profiles/r04/ab/fabrik_refill_prio_prep_carry.txt.)
+// (r04: taking the seed's carried quotient in the prepare step instead of at the
+// hand-out measured slower, profiles/r04/ab/fabrik_refill_prio_prep_carry.txt; r06
+// takes it there as part of a bundle that measured faster, DESIGN_HISTORY.md.)
 constexpr int kIterWaves = IKHIP_ITER_WAVES;  // waves per SIMD = blocks per CU
 template <int REFILL_MIN, bool ORD, int CORE>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kIterWaves, kIterWaves))) void
@@ -1187,9 +1189,10 @@ fabrik_iter_kernel(FabArgs a) {
         cont = true;  // the loop's initial errors of 1.0 (fabrik.py:53-54) exceed tol
         kst = 0u - (uint32_t)max_iter;
         active = true;
-        // (CORE 2: the carry and the band flag came with the entry, take_entry; a
-        // carry outside the core domain stops the lane before its first iteration,
-        // for the retire step's re-solve)
+        // (CORE 2: the carry came with the entry, take_entry; an entry the
+        // preparation sent to the re-solve -- its carry outside the core domain,
+        // or its goal past the band -- stops before its first iteration, for the
+        // retire step's solve_general)
         if constexpr (CORE == 2) {
           if (cbad) {
             st = kStRedo;
