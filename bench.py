@@ -138,6 +138,50 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def open_sharded(ctx, world, rank, sharded=None, unique_id=None):
+    """The library's RCCL communicator for the timed steps' all-gather (SURVEY
+    §8(e)), or -- when RCCL is missing or its init fails (or times out) on ANY
+    rank -- None on every rank, with the reason: the ranks then solve their shards
+    with no collective (the survey's host-only fallback) and the line says so
+    (config.all_gather_in_step false, config.rccl_fallback), instead of the run
+    dying.  The ranks agree over the gloo control plane.  sharded / unique_id:
+    dist.ShardedContext and _native.comm_unique_id, replaceable by tests."""
+    import torch
+    import torch.distributed as dist
+    from inversekinematicsann_amd import _native
+    from inversekinematicsann_amd import dist as D
+    sharded = sharded or D.ShardedContext
+    unique_id = unique_id or _native.comm_unique_id
+    sc, why = None, None
+    uid = None
+    if rank == 0:
+        try:
+            uid = unique_id()
+        except Exception as e:  # (no RCCL library, or ncclGetUniqueId failed)
+            why = f"{type(e).__name__}: {e}"
+    uid = D.torch_broadcast(uid)  # None on every rank when rank 0 has no id
+    if uid is None:
+        why = why or "rank 0 has no RCCL unique id"
+    else:
+        try:
+            sc = sharded(ctx, world, rank, uid)
+        except Exception as e:  # (init failed, or the library's deadline aborted it)
+            why = f"{type(e).__name__}: {e}"
+    ok = torch.tensor([0 if sc is None else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        if sc is not None:
+            try:
+                sc.close()
+            except Exception:  # (its peers never joined: nothing to tear down cleanly)
+                pass
+            sc = None
+        why = why or "another rank's RCCL init failed"
+        print(f"bench.py: rank {rank}: RCCL unavailable ({why}); the ranks solve their "
+              f"shards with no collective", file=sys.stderr)
+    return sc, why
+
+
 def dist_setup(args):
     """One process per GPU.  torch.distributed (gloo, CPU) is the control plane
     only; the data path is the library's RCCL communicator (dist.ShardedContext)."""
@@ -1147,9 +1191,9 @@ def main():
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    sc = None
+    sc, rccl_fallback = None, None
     if world > 1 and args.gather:
-        sc = D.ShardedContext(ctx, world, rank, D.exchange_unique_id(rank, D.torch_broadcast))
+        sc, rccl_fallback = open_sharded(ctx, world, rank)
     job = Job(ctx, sc, pts, dpts, lo, hi, world)
     other_modes = [m for m in ("fp32", "bf16x6", "fp16x3") if m != args.ann_mode]
     runners = {"ann": lambda j, a: run_ann(j, a, mode=args.ann_mode), "fabrik": run_fabrik,
@@ -1206,6 +1250,7 @@ def main():
                    **({"devices_shared": world // max(1, torch.cuda.device_count())}
                       if world > torch.cuda.device_count() else {}),
                    "all_gather_in_step": sc is not None,
+                   **({"rccl_fallback": rccl_fallback} if rccl_fallback else {}),
                    "collective": ("RCCL all-gathers inside libikhip (ik_*_solve_sharded): each "
                                   "chunk's angles (+ FABRIK iterations) gathered in place under "
                                   "the next chunk's solve; per-rank stats tail + FK-error "

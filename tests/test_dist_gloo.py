@@ -340,3 +340,65 @@ def test_world8_lowest_failing_index():
             assert st["first_oob"] == 2950
             assert st["first_err"] == 3001 and st["first_err_code"] == 3
             assert np.isnan(ang[3001]).all() and np.isnan(ang[7100]).all()
+
+
+def _fallback_worker(rank, world, port, case, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world))
+    import sys
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        closed = []
+
+        class FakeSharded:
+            def __init__(self, ctx, w, r, uid):
+                if case == "init_fails_on_1" and r == 1:
+                    raise RuntimeError("IK_E_RCCL: ncclCommInitRankConfig timed out")
+                self.uid = uid
+
+            def close(self):
+                closed.append(True)
+
+        def uid():
+            if case == "no_rccl":
+                raise OSError("librccl.so: cannot open shared object file")
+            return b"\x01" * 128
+
+        sc, why = bench.open_sharded(None, world, rank, sharded=FakeSharded, unique_id=uid)
+        q.put((rank, sc is not None, why, bool(closed), getattr(sc, "uid", None)))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, "error", repr(e), False, None))
+
+
+@pytest.mark.parametrize("case", ["ok", "no_rccl", "init_fails_on_1"])
+def test_bench_rccl_fallback_agreed_by_every_rank(case):
+    """SURVEY §8(e)'s host-only fallback: when RCCL is missing on rank 0 or its init
+    fails on one rank, bench.open_sharded gives every rank no communicator (the ranks
+    agree over gloo; a rank whose own init succeeded closes it) and the reason, so
+    the N > 1 line runs with no collective instead of dying; with RCCL working every
+    rank gets the communicator built from rank 0's broadcast id."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fallback_worker, args=(r, world, port, case, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+    assert all(r[1] != "error" for r in res), res
+    if case == "ok":
+        assert all(r[1] is True and r[2] is None and r[4] == b"\x01" * 128 for r in res)
+    else:
+        assert all(r[1] is False and r[2] for r in res), res
+        if case == "no_rccl":
+            assert all("librccl" in r[2] or "unique id" in r[2] for r in res)
+        else:
+            assert res[0][3] is True  # rank 0's own communicator was closed
+            assert "timed out" in res[1][2] and "another rank" in res[0][2]
