@@ -537,13 +537,14 @@ def run_ann(job, args, mode="fp32"):
             (BF16_MFMA_PEAK if mode == "bf16x6" else FP16_MFMA_PEAK) / SPLIT_PRODUCTS[mode])
     traffic = load_traffic(args.traffic_file, kname)
     prof = profile_fields(args.traffic_file, kname)
-    fr = roofline_fracs(flop_pt * n, k, peak, prof, res["ms_per_step"])
+    fr = roofline_fracs(flop_pt * n, k, peak, prof, res["event_step_ms"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
                        "peak": peak / 1e12, "unit": "TFLOP/s",
                        "frac": achieved / peak if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
+                       "event_step_ms": res["event_step_ms"],
                        "traffic": traffic, "kernel": kname,
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
                        "points_per_launch": n, **prof}
@@ -663,13 +664,14 @@ def run_fabrik(job, args, tol=None, max_iter=None):
         "fabrik_tol1e-5/fabrik_iter_kernel"
     traffic = load_traffic(args.traffic_file, pkey)
     prof = profile_fields(args.traffic_file, pkey)
-    fr = roofline_fracs(flops, k, FP64_VALU_PEAK, prof, res["ms_per_step"])
+    fr = roofline_fracs(flops, k, FP64_VALU_PEAK, prof, res["event_step_ms"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "valu_fp64", "achieved": achieved / 1e12 if achieved else None,
                        "peak": FP64_VALU_PEAK / 1e12, "unit": "TFLOP/s",
                        "frac": achieved / FP64_VALU_PEAK if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
+                       "event_step_ms": res["event_step_ms"],
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
                        "algorithmic_flop_per_point": FABRIK_FLOP_PER_POINT,
@@ -691,17 +693,18 @@ def run_fabrik(job, args, tol=None, max_iter=None):
 FK_BYTES_PER_POINT = 32 + 24   # float64 angles in, float64 effector xyz out
 
 
-FK_BATCH_FACTOR = 8  # FK angle vectors per rank = 8 x the shard's points (8M at the default)
+FK_BATCH_FACTOR = 32  # FK angle vectors per rank = 32 x the shard's points (32M at the default)
 
 
 def run_fk(job, args):
     """Batched FK (forward.py:73-94, the DH chain) on
     FK_BATCH_FACTOR times as many angle vectors as this rank's shard has points,
     drawn uniformly in [-pi, pi): its bound is HBM (56 B per point) or the float64
-    sin/cos + products, whichever is longer.  8M vectors make a launch ~0.1 ms, so
-    the dispatch's fixed ~1 us (completion signal) is < 1 % of the kernel time the
-    roofline divides by (at 1M it was 7 %, r06 lease A).  No collective (each rank
-    its own vectors)."""
+    sin/cos + products, whichever is longer.  32M vectors (1.8 GB per launch) make
+    a launch ~0.36 ms and are ~7x the 256 MB Infinity Cache, so no step re-reads the
+    last one's angles from it: at 8M (448 MB) the events-timed loop ran ~7 % faster
+    than rocprof's serialized dispatches, at 1M the dispatch's fixed cost was 7 %
+    (r06).  No collective (each rank its own vectors)."""
     import torch
     from inversekinematicsann_amd import _native
     ctx, world, n = job.ctx, job.world, job.n_local * FK_BATCH_FACTOR
@@ -718,13 +721,14 @@ def run_fk(job, args):
     res["outputs"] = {"xyz": dxyz}
     k = res["kernels"].get("fk_kernel")
     prof = profile_fields(args.traffic_file, "fk_kernel")
-    fr = roofline_fracs(FK_BYTES_PER_POINT * n, k, HBM_PEAK, prof, res["ms_per_step"])
+    fr = roofline_fracs(FK_BYTES_PER_POINT * n, k, HBM_PEAK, prof, res["event_step_ms"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None,
                        "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                        "frac": achieved / HBM_PEAK if achieved else None,
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
+                       "event_step_ms": res["event_step_ms"],
                        "kernel_ms_note": "events: the dispatch's own start / end stamps "
                                          "(hipExtLaunchKernel); rocprof: its kernel trace",
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
@@ -764,12 +768,18 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
     # step is enqueued right behind an untimed one, as in the timed loop (a step
     # from an idle queue ran its kernels 3-6 % slower than the loop's); median of
     # TIMING_REPS such steps.
-    per = {}
+    per, steps_ms = {}, []
     for _ in range(TIMING_REPS):
         step()
         ctx.set_timing(True)
+        s0 = torch.cuda.Event(enable_timing=True)
+        s1 = torch.cuda.Event(enable_timing=True)
+        s0.record()
         step()
+        s1.record()
         ctx.sync()
+        torch.cuda.synchronize()
+        steps_ms.append(s0.elapsed_time(s1))
         one = {}
         for name, ms in ctx.kernel_times():
             one[name] = one.get(name, 0.0) + ms
@@ -777,6 +787,11 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
         for name, ms in one.items():
             per.setdefault(name, []).append(ms)
     kernels = {name: float(np.median(v)) for name, v in per.items()}
+    # the event-timed steps' own durations (the same stream's events around each):
+    # a kernel's duration must fit inside the step it was stamped in -- the timed
+    # loop's mean below can come out a hair shorter than a kernel that is ~all of
+    # the step, from run-to-run clock drift alone
+    event_step_ms = float(np.median(steps_ms))
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -795,7 +810,7 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
     wall = max_over_ranks(wall, world)
     ev_ms = ev0.elapsed_time(ev1) / args.steps
     return {"wall_s": wall, "ms_per_step": wall * 1e3 / args.steps, "event_ms_per_step": ev_ms,
-            "kernels": kernels}
+            "kernels": kernels, "event_step_ms": event_step_ms}
 
 
 def cold_steps(ctx, step, reps=3):
@@ -1101,7 +1116,7 @@ def secondary_entry(key, r2, total, world, args):
 DRIVER_TIMEOUT_S = 600  # the driver's limit on one bench.py run (BENCH_r05.json timeout_s)
 # measured per-step times at 1M points per rank (profiles/r05/lease_bench_default.json)
 LEG_STEP_MS = {"ann": 39.2, "fabrik": 0.36, "fabrik_tol1e-5": 0.51, "ann_bf16x6": 21.9,
-               "ann_fp16x3": 12.7, "fk": 0.13}  # (fk: FK_BATCH_FACTOR x the points)
+               "ann_fp16x3": 12.7, "fk": 0.45}  # (fk: FK_BATCH_FACTOR x the points)
 E2E_BYTES_PER_POINT = {"ann": 24 + 16, "fabrik": 24 + 32}
 PCIE_BYTES_PER_S = 50e9   # tools/pcie_probe.py: ~55 GB/s, the directions do not overlap
 STARTUP_S = 120.0         # first `import torch` + HIP init on a fresh box (1-2 min)
