@@ -50,7 +50,8 @@ FP64_VALU_PEAK = 78.6e12    # MI355X fp64 vector peak (spec)
 HBM_PEAK = 8.0e12           # bytes/s
 FABRIK_FLOP_PER_ITER = 132  # per executed reference iteration
 FABRIK_FLOP_PER_POINT = 150  # + the seed FK and angles, per point
-TIMING_REPS = 5             # single steps timed per kernel (median)
+TIMING_REPS = 5              # steps timed per kernel (median)
+TIMING_LEAD = 2              # steps ahead of them in the same back-to-back run, not used
 
 
 def launch_command(argv, gpus, port):
@@ -291,23 +292,33 @@ def kernel_time_ok(kernel_ms, step_ms):
     return bool(kernel_ms) and bool(step_ms) and kernel_ms <= step_ms
 
 
-def roofline_fracs(work, kernel_ms, peak, prof, step_ms=None):
+def roofline_fracs(work, kernel_ms, peak, prof, step_ms=None, loop_ms=None):
     """The roofline's achieved rate both ways: from this run's
     HIP-event kernel time (the dispatch's own start / end stamps) and from the
     committed rocprof window average of the same kernel (`prof`:
     profile_fields); `frac` / `achieved` headline the LOWER of the two.  An
-    events duration longer than the step (`step_ms`, kernel_time_ok) is not a
-    kernel duration and is dropped.  work: algorithmic flop (or bytes) per launch."""
+    events duration is a kernel duration only if it fits inside the step it was
+    stamped in (`step_ms`, kernel_time_ok) and inside the untimed loop's step
+    (`loop_ms`, 1 % for clock drift): the event-stamped launch of a short
+    memory-bound kernel can run slower than the untimed loop (FK: ~9 %, r06), and
+    then rocprof's window stands alone.  work: algorithmic flop (or bytes) per launch."""
     valid = kernel_time_ok(kernel_ms, step_ms) if step_ms is not None else bool(kernel_ms)
+    note = None
+    if valid and loop_ms is not None and kernel_ms > 1.01 * loop_ms:
+        valid, note = False, ("the event-stamped launch ran longer than the untimed loop's "
+                              "step: the rocprof window alone prices the roofline")
     ev = work / (kernel_ms / 1e3) if valid else None
     rp = prof.get("rocprof_avg_ms")
     rq = work / (rp / 1e3) if rp else None
     cands = [x for x in (ev, rq) if x]
     head = min(cands) if cands else None
-    return {"achieved_events": ev, "frac_events": ev / peak if ev else None,
-            "achieved_rocprof": rq, "frac_rocprof": rq / peak if rq else None,
-            "headline": None if head is None else ("rocprof" if head == rq else "events"),
-            "kernel_ms_valid": valid, "_head": head}
+    out = {"achieved_events": ev, "frac_events": ev / peak if ev else None,
+           "achieved_rocprof": rq, "frac_rocprof": rq / peak if rq else None,
+           "headline": None if head is None else ("rocprof" if head == rq else "events"),
+           "kernel_ms_valid": valid, "_head": head}
+    if note:
+        out["kernel_ms_note"] = note
+    return out
 
 
 def load_pipe(path, kernel):
@@ -537,7 +548,7 @@ def run_ann(job, args, mode="fp32"):
             (BF16_MFMA_PEAK if mode == "bf16x6" else FP16_MFMA_PEAK) / SPLIT_PRODUCTS[mode])
     traffic = load_traffic(args.traffic_file, kname)
     prof = profile_fields(args.traffic_file, kname)
-    fr = roofline_fracs(flop_pt * n, k, peak, prof, res["event_step_ms"])
+    fr = roofline_fracs(flop_pt * n, k, peak, prof, res["event_step_ms"], res["ms_per_step"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "mfma", "achieved": achieved / 1e12 if achieved else None,
                        "peak": peak / 1e12, "unit": "TFLOP/s",
@@ -545,6 +556,7 @@ def run_ann(job, args, mode="fp32"):
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
                        "event_step_ms": res["event_step_ms"],
+                       **({"kernel_ms_note": fr["kernel_ms_note"]} if "kernel_ms_note" in fr else {}),
                        "traffic": traffic, "kernel": kname,
                        "kernel_ms": k, "algorithmic_flop_per_point": flop_pt,
                        "points_per_launch": n, **prof}
@@ -664,7 +676,7 @@ def run_fabrik(job, args, tol=None, max_iter=None):
         "fabrik_tol1e-5/fabrik_iter_kernel"
     traffic = load_traffic(args.traffic_file, pkey)
     prof = profile_fields(args.traffic_file, pkey)
-    fr = roofline_fracs(flops, k, FP64_VALU_PEAK, prof, res["event_step_ms"])
+    fr = roofline_fracs(flops, k, FP64_VALU_PEAK, prof, res["event_step_ms"], res["ms_per_step"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "valu_fp64", "achieved": achieved / 1e12 if achieved else None,
                        "peak": FP64_VALU_PEAK / 1e12, "unit": "TFLOP/s",
@@ -672,6 +684,7 @@ def run_fabrik(job, args, tol=None, max_iter=None):
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
                        "event_step_ms": res["event_step_ms"],
+                       **({"kernel_ms_note": fr["kernel_ms_note"]} if "kernel_ms_note" in fr else {}),
                        "traffic": traffic, "kernel": "fabrik_iter_kernel", "kernel_ms": k,
                        "algorithmic_flop_per_iteration": FABRIK_FLOP_PER_ITER,
                        "algorithmic_flop_per_point": FABRIK_FLOP_PER_POINT,
@@ -721,7 +734,8 @@ def run_fk(job, args):
     res["outputs"] = {"xyz": dxyz}
     k = res["kernels"].get("fk_kernel")
     prof = profile_fields(args.traffic_file, "fk_kernel")
-    fr = roofline_fracs(FK_BYTES_PER_POINT * n, k, HBM_PEAK, prof, res["event_step_ms"])
+    fr = roofline_fracs(FK_BYTES_PER_POINT * n, k, HBM_PEAK, prof, res["event_step_ms"],
+                        res["ms_per_step"])
     achieved = fr.pop("_head")
     res["roofline"] = {"bound": "hbm", "achieved": achieved / 1e9 if achieved else None,
                        "peak": HBM_PEAK / 1e9, "unit": "GB/s",
@@ -729,6 +743,7 @@ def run_fk(job, args):
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
                        "event_step_ms": res["event_step_ms"],
+                       **({"kernel_ms_note": fr["kernel_ms_note"]} if "kernel_ms_note" in fr else {}),
                        "kernel_ms_note": "events: the dispatch's own start / end stamps "
                                          "(hipExtLaunchKernel); rocprof: its kernel trace",
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
@@ -764,34 +779,59 @@ def timed(ctx, step, args, world, warm=None, after_warm=None):
     # per-kernel durations: the library launches each kernel of a timed call with
     # hipExtLaunchKernel's start / stop events, which the dispatch itself stamps
     # (ik_ctx_set_timing), so a kernel's interval holds neither the
-    # kernels ahead of it in the step nor the host's launch latency.  Each timed
-    # step is enqueued right behind an untimed one, as in the timed loop (a step
-    # from an idle queue ran its kernels 3-6 % slower than the loop's); median of
-    # TIMING_REPS such steps.
-    per, steps_ms = {}, []
-    for _ in range(TIMING_REPS):
-        step()
-        ctx.set_timing(True)
+    # kernels ahead of it in the step nor the host's launch latency.  TIMING_LEAD +
+    # TIMING_REPS steps back to back with the timings accumulating (set_timing(2):
+    # no host sync between them, so no step starts from an idle, clocked-down GPU --
+    # a 0.4 ms FK step behind a single lead step still ran ~5 % slow); the median
+    # of the last TIMING_REPS steps' per-kernel sums, each step's own duration from
+    # the stream's events around it.
+    kernels, event_step_ms = {}, None
+    nsteps = TIMING_LEAD + TIMING_REPS
+    ctx.set_timing(2)
+    evs = []
+    for _ in range(nsteps):
         s0 = torch.cuda.Event(enable_timing=True)
         s1 = torch.cuda.Event(enable_timing=True)
         s0.record()
         step()
         s1.record()
-        ctx.sync()
-        torch.cuda.synchronize()
-        steps_ms.append(s0.elapsed_time(s1))
-        one = {}
-        for name, ms in ctx.kernel_times():
-            one[name] = one.get(name, 0.0) + ms
-        ctx.set_timing(False)
-        for name, ms in one.items():
-            per.setdefault(name, []).append(ms)
-    kernels = {name: float(np.median(v)) for name, v in per.items()}
-    # the event-timed steps' own durations (the same stream's events around each):
-    # a kernel's duration must fit inside the step it was stamped in -- the timed
-    # loop's mean below can come out a hair shorter than a kernel that is ~all of
-    # the step, from run-to-run clock drift alone
-    event_step_ms = float(np.median(steps_ms))
+        evs.append((s0, s1))
+    ctx.sync()
+    torch.cuda.synchronize()
+    times = ctx.kernel_times()
+    ctx.set_timing(False)
+    if times and len(times) % nsteps == 0 and len(times) < 64:
+        per_step = len(times) // nsteps
+        per = {}
+        for s_ in range(TIMING_LEAD, nsteps):
+            one = {}
+            for name, ms in times[s_ * per_step:(s_ + 1) * per_step]:
+                one[name] = one.get(name, 0.0) + ms
+            for name, ms in one.items():
+                per.setdefault(name, []).append(ms)
+        kernels = {name: float(np.median(v)) for name, v in per.items()}
+        event_step_ms = float(np.median([a.elapsed_time(b) for a, b in evs[TIMING_LEAD:]]))
+    else:  # (more kernels a step than the 64 slots hold: each step timed on its own)
+        per, steps_ms = {}, []
+        for _ in range(TIMING_REPS):
+            step()
+            ctx.set_timing(True)
+            s0 = torch.cuda.Event(enable_timing=True)
+            s1 = torch.cuda.Event(enable_timing=True)
+            s0.record()
+            step()
+            s1.record()
+            ctx.sync()
+            torch.cuda.synchronize()
+            steps_ms.append(s0.elapsed_time(s1))
+            one = {}
+            for name, ms in ctx.kernel_times():
+                one[name] = one.get(name, 0.0) + ms
+            ctx.set_timing(False)
+            for name, ms in one.items():
+                per.setdefault(name, []).append(ms)
+        kernels = {name: float(np.median(v)) for name, v in per.items()}
+        event_step_ms = float(np.median(steps_ms))
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
@@ -1127,7 +1167,7 @@ BATCH_GEN_S_PER_M = 0.2   # random_dist, seconds per million points (1.4 s for 1
 def wall_budget(world, steps, warmup, rccl_timeout_s=120.0, points=1_000_000, cpu_seconds=10.0):
     """An upper estimate of one `bench.py --gpus N` run's wall time, in seconds,
     by leg (the driver's first N = 8 run must fit its 600 s
-    limit).  Each leg: W warm-up + TIMING_REPS event-timed + K timed steps, the
+    limit).  Each leg: W warm-up + TIMING_LEAD + TIMING_REPS event-timed + K timed steps, the
     untimed gather check (N > 1: two parts re-solved), 20 end-to-end calls each
     way (pinned / pageable, the whole batch through PCIe), and its batch
     generation; plus start-up, RCCL init and, at N > 1, the two strong legs on
@@ -1137,7 +1177,7 @@ def wall_budget(world, steps, warmup, rccl_timeout_s=120.0, points=1_000_000, cp
     per_rank_m = points / 1e6
     legs = {}
     for key, ms in LEG_STEP_MS.items():
-        n_steps = warmup + TIMING_REPS + steps + (2 if world > 1 else 0)
+        n_steps = warmup + TIMING_LEAD + TIMING_REPS + steps + (2 if world > 1 else 0)
         t = n_steps * ms * per_rank_m / 1e3
         method = "fabrik" if key.startswith("fabrik") else ("ann" if key.startswith("ann") else None)
         if method:
@@ -1149,7 +1189,7 @@ def wall_budget(world, steps, warmup, rccl_timeout_s=120.0, points=1_000_000, cp
     if world > 1:
         sm = STRONG_POINTS / world / 1e6
         for key, base in (("ann_strong10M", "ann"), ("fabrik_tol1e-5_strong10M", "fabrik_tol1e-5")):
-            n_steps = warmup + TIMING_REPS + steps + 2
+            n_steps = warmup + TIMING_LEAD + TIMING_REPS + steps + 2
             legs[key] = (n_steps * LEG_STEP_MS[base] * sm / 1e3
                          + BATCH_GEN_S_PER_M * STRONG_POINTS / 1e6
                          + (BATCH_GEN_S_PER_M * STRONG_POINTS / 1e6 if base.startswith("fabrik")

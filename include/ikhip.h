@@ -200,10 +200,12 @@ int ik_ann_effective_mode(ik_ctx *ctx);
  * goes through hipExtLaunchKernel with a start and a stop event, which the
  * dispatch itself stamps (the kernel's own start and end: not the kernels ahead
  * of it on the stream, not the host's launch latency); the RCCL gather of a
- * sharded call is bracketed by stream markers.  ik_kernel_times
- * waits for the last call's events and returns how many kernels it timed,
- * their durations in ms and (if names != NULL) their names, name_len bytes
- * each; a negative value is -ik_status. */
+ * sharded call is bracketed by stream markers.  on = 1: ik_kernel_times
+ * returns the last call's kernels; on = 2: the calls' kernels accumulate, in
+ * launch order, up to 64, until the next ik_ctx_set_timing (back-to-back calls
+ * timed with no host sync between them).  ik_kernel_times waits for the events
+ * and returns how many kernels were timed, their durations in ms and (if names
+ * != NULL) their names, name_len bytes each; a negative value is -ik_status. */
 int ik_ctx_set_timing(ik_ctx *ctx, int on);
 int ik_kernel_times(ik_ctx *ctx, int max, float *ms, char *names, int name_len);
 

@@ -572,11 +572,14 @@ class Context:
             ctypes.byref(s))))
         return s
 
-    def set_timing(self, on: bool = True):
-        self._check(self.lib.ik_ctx_set_timing(self.handle, 1 if on else 0))
+    def set_timing(self, on=True):
+        """ik_ctx_set_timing: True / 1 each call's kernels, 2 accumulate across calls
+        (up to 64 kernels, in launch order), False / 0 off."""
+        self._check(self.lib.ik_ctx_set_timing(self.handle, 2 if on == 2 else (1 if on else 0)))
 
     def kernel_times(self):
-        """[(kernel name, ms)] of the last call (after set_timing(True))."""
+        """[(kernel name, ms)] of the last call (after set_timing(True)), or of every
+        call since set_timing(2), in launch order."""
         ms = np.zeros(64, np.float32)
         names = ctypes.create_string_buffer(64 * 48)
         n = self.lib.ik_kernel_times(self.handle, 64, ms.ctypes.data, ctypes.addressof(names), 48)

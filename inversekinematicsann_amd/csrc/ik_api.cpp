@@ -115,7 +115,7 @@ int fail(int code, const std::string &msg) {
 
 KtScope::KtScope(ik_ctx *c) : c_(c) {
   g_kt = &c->kt;
-  c->kt.n = 0;
+  if (!c->kt.acc) c->kt.n = 0;  // (accumulating: slots fill across calls, up to kMaxTimed)
   c->kt.state = 0;
   // calls on one context share its stats block and work-queue words: a call on
   // another stream than the last one starts after that one's work
@@ -406,6 +406,7 @@ int ik_ctx_set_timing(ik_ctx *c, int on) {
     }
   }
   c->kt.on = on != 0;
+  c->kt.acc = on == 2;
   c->kt.n = 0;
   c->kt.state = 0;
   return IK_OK;

@@ -15,6 +15,7 @@ namespace ikhip {
 constexpr int kMaxTimed = 64;  // kernels timed per call (the layered ANN path launches one per layer)
 struct KTimer {
   bool on = false;
+  bool acc = false;  // ik_ctx_set_timing(ctx, 2): the calls' kernels accumulate
   int n = 0;
   // slot n's state: 1 = armed by kt_begin (the next IK_LAUNCH takes its events),
   // 2 = stamped by that dispatch, 3 = a marker span (kt_span_begin)

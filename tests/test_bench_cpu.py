@@ -202,6 +202,19 @@ def test_strong_legs_are_configs_3_and_4_at_world_8():
         assert bench._config_ref("fabrik", 10_000_000, w, 1e-5, 200) == "configs[4]"
 
 
+def test_kernel_duration_longer_than_the_untimed_loop_is_dropped():
+    """An events duration that fits its own event-timed step but exceeds the untimed
+    loop's step by more than 1 % (the event-stamped launch ran slower: FK, r06) is
+    not priced: the rocprof window stands alone, and the line says why."""
+    import bench
+    prof = {"rocprof_avg_ms": 0.407}
+    fr = bench.roofline_fracs(1.0e9, 0.452, 8e12, prof, step_ms=0.47, loop_ms=0.413)
+    assert not fr["kernel_ms_valid"] and fr["frac_events"] is None and "kernel_ms_note" in fr
+    assert fr["headline"] == "rocprof"
+    fr = bench.roofline_fracs(1.0e9, 21.55, 8e12, prof, step_ms=21.57, loop_ms=21.52)
+    assert fr["kernel_ms_valid"] and "kernel_ms_note" not in fr
+
+
 def test_kernel_duration_longer_than_its_step_is_dropped():
     """an events duration longer than the step that launched the
     kernel is not a kernel duration; the roofline then rests on rocprof alone."""
@@ -252,8 +265,10 @@ def test_committed_bench_lines_kernel_fits_step():
             if k is None or step is None:
                 continue
             own = rf.get("event_step_ms")
+            if own is not None and rf.get("kernel_ms_valid") is False:
+                continue  # (dropped by the line itself: kernel_ms_note says why)
             assert k <= (own if own is not None else step), (path, name, k, own, step)
-            assert k <= step * 1.005, (path, name, k, step)
+            assert k <= step * 1.01, (path, name, k, step)
             fe, fr = rf.get("frac_events"), rf.get("frac_rocprof")
             # (against a rocprof profile of this round's kernels only)
             same_round = str(rf.get("profile", "")).startswith("profiles/r06")
