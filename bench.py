@@ -743,9 +743,9 @@ def run_fk(job, args):
                        "frac_events": fr["frac_events"], "frac_rocprof": fr["frac_rocprof"],
                        "frac_headline": fr["headline"], "kernel_ms_valid": fr["kernel_ms_valid"],
                        "event_step_ms": res["event_step_ms"],
+                       "timing_note": "events: the dispatch's own start / end stamps "
+                                      "(hipExtLaunchKernel); rocprof: its kernel trace",
                        **({"kernel_ms_note": fr["kernel_ms_note"]} if "kernel_ms_note" in fr else {}),
-                       "kernel_ms_note": "events: the dispatch's own start / end stamps "
-                                         "(hipExtLaunchKernel); rocprof: its kernel trace",
                        "traffic": load_traffic(args.traffic_file, "fk_kernel"),
                        **prof,
                        "kernel": "fk_kernel", "kernel_ms": k,
